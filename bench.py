@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X fractal ray-marcher.
+
+Workload (BASELINE.json metric): 3840x2160 Mandelbulb (scene 18 at power 8), 12 DE
+iterations, 256 march steps, fixed camera pose P1; one "step" = one whole frame of the
+hot path (fragment_main for every pixel) with inputs resident on the GPU. N GPUs
+row-tile the same frame (interleaved bands, strong scaling) and gather it to rank 0
+over RCCL, then rank 0 reassembles it (frm_unshuffle_bands).
+
+Prints ONE JSON line on rank 0. `value` = G ray-march-steps/s of the whole job
+(primary + shadow march() iterations, counted exactly by the kernel, / wall time).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload HEADLINE|C2|C3|C4|C5]
+                    [--pose P0|P1|P2] [--kernel persistent|simple] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "fractal-ray-marching_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+# Peak VALU issue of MI355X: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (f32 lane-ops/s;
+# = 157.3 TFLOP/s counting an FMA as 2), /opt/skills/guides/MI355X_MICROARCH.md.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+METRIC = "Gray-march-steps/sec + frames/sec, 4K Mandelbulb 12-iter/256-step, 1 & 8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="HEADLINE")
+    ap.add_argument("--pose", default="P1")
+    ap.add_argument("--kernel", default="persistent", choices=["persistent", "simple"])
+    ap.add_argument("--band-rows", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(params, w, seconds):
+    """Oracle (C restatement, thread pool with a dynamic row queue) on a bounded,
+    evenly spaced row sample of the same frame; steps/s extrapolates per step."""
+    from oracle import frm_oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    flags = 1 if w.sphere else 0
+    # calibration: 8 evenly spaced rows
+    stride = max(1, w.height // 8)
+    rows = list(range(stride // 2, w.height, stride))
+    t0 = time.perf_counter()
+    r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows, threads=threads)
+    dt = time.perf_counter() - t0
+    per_row = dt / len(rows)
+    n = int(max(len(rows), min(w.height, seconds / max(per_row, 1e-9))))
+    if n > len(rows):
+        stride = max(1, w.height // n)
+        rows = list(range(stride // 2, w.height, stride))
+        t0 = time.perf_counter()
+        r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows,
+                              threads=threads)
+        dt = time.perf_counter() - t0
+    c = r["counters"]
+    steps = int(c[2]) + int(c[3])
+    return {
+        "value": steps / dt / 1e9,
+        "unit": "Gray-march-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{len(rows)} evenly spaced rows (every {stride}th) of the {w.width}x{w.height} frame, "
+                  f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O2, {threads} threads",
+        "frames_per_s_extrapolated": (len(rows) / w.height) / dt,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import frm
+    from frm import tiling
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N>1 with torch.distributed.run)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    w = frm.WORKLOADS[args.workload]
+    params = frm.make_parameters(w, pose=args.pose)
+    flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
+        frm.FRM_FLAG_SIMPLE_KERNEL if args.kernel == "simple" else 0)
+    r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags)
+    r.resize(w.width, w.height)
+    r.update_parameters_buffer(params)
+
+    band_rows = args.band_rows or (w.height if world == 1 else tiling.choose_band_rows(w.height, world))
+    rows_local = tiling.rank_buffer_rows(w.height, band_rows, world)
+    nbytes = rows_local * w.width * 4
+    dev = torch.device("cuda", local)
+    bufs = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2 if world > 1 else 1)]
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    frame = gathered = None
+    if world > 1 and rank == 0:
+        gathered = [torch.empty(world * nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        frame = torch.empty(w.height * w.width * 4, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+
+    def render(k, timed):
+        buf = bufs[k % len(bufs)]
+        if timed:
+            kev[k][0].record(stream)
+        r.render_bands(buf.data_ptr(), nbytes, band_rows, rank, world, stream.cuda_stream,
+                       counters.data_ptr())
+        if timed:
+            kev[k][1].record(stream)
+        if world == 1:
+            return None
+        glist = None
+        if rank == 0:
+            g = gathered[k % 2]
+            glist = [g[i * nbytes:(i + 1) * nbytes] for i in range(world)]
+        return dist.gather(buf, gather_list=glist, dst=0, async_op=True)
+
+    def finish(k, work):
+        if work is None:
+            return
+        work.wait()
+        if rank == 0:
+            r.unshuffle_bands(gathered[k % 2].data_ptr(), nbytes, frame.data_ptr(), frame.numel(),
+                              band_rows, world, stream.cuda_stream)
+
+    def run(n, timed):
+        pending = None
+        for k in range(n):
+            work = render(k, timed)
+            if pending is not None:
+                finish(*pending)
+            pending = (k, work)
+        if pending is not None:
+            finish(*pending)
+
+    run(args.warmup, False)
+    torch.cuda.synchronize()
+    counters.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in kev)
+
+    stats_vec = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    cnt = counters.clone()
+    if world > 1:
+        dist.all_reduce(stats_vec[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    elapsed = float(stats_vec[0])
+    c = [int(v) for v in cnt.cpu().tolist()]
+    st = r.stats_from_counters(c)
+    steps_total = st["march_steps"]
+    if rank == 0:
+        avg_kernel_s = kernel_ms / 1e3 / args.steps
+        wom_per_launch = st["wom_ops"] / args.steps / world
+        achieved = wom_per_launch / avg_kernel_s / 1e12
+        out = {
+            "metric": METRIC,
+            "value": steps_total / elapsed / 1e9,
+            "unit": "Gray-march-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: deterministic Parameters (fixed camera pose, fixed time), no input data",
+            "config": {
+                "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
+                "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
+                "pose": args.pose, "kernel": args.kernel,
+                "parallelism": f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if world > 1
+                               else "single GPU",
+            },
+            "frames_per_sec": args.steps / elapsed,
+            "march_steps_per_frame": steps_total / args.steps,
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": VALU_PEAK_TOPS,
+                "unit": "Tlane-op/s",
+                "frac": achieved / VALU_PEAK_TOPS,
+                "traffic": None,
+                "kernel": "frm::render",
+                "avg_kernel_ms": avg_kernel_s * 1e3,
+                "algorithmic_ops_per_launch": wom_per_launch,
+                "model": "WOM VALU lane-ops counted from fragment.wgsl (DESIGN.md §Roofline)",
+            },
+            "counters": st,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(params, w, args.cpu_seconds)
+        print(json.dumps(out))
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

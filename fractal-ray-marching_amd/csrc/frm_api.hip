@@ -1,0 +1,348 @@
+// frm_api.hip — the C ABI of include/frm.h: context lifetime, device buffers, uniform
+// upload, frame dispatch and readback. Replaces the reference's wgpu host layer
+// (graphics.rs:25-164, persistent_graphics.rs:33-173, blit_graphics.rs:16-62).
+// Errors never cross the ABI as exceptions/aborts: every HIP failure becomes a status
+// code plus a message retrievable with frm_last_error().
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "frm.h"
+#include "frm_internal.h"
+
+using namespace frm;
+
+struct frm_ctx {
+  int device = 0;
+  uint32_t max_steps = FRM_DEFAULT_MAX_STEPS;
+  uint32_t flags = 0;
+  int cu_count = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  uint32_t width = 0, height = 0;
+  uint8_t* fb = nullptr;
+  unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
+  unsigned int* queue = nullptr;
+  frm_parameters params{};
+  bool has_params = false;
+  SceneUniforms scene{};
+  std::string error;
+};
+
+namespace {
+
+thread_local std::string g_error;  // failures without a context
+
+int fail(frm_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->error = buf;
+  g_error = buf;
+  return code;
+}
+
+int hip_fail(frm_ctx* ctx, hipError_t e, const char* what) {
+  int code = (e == hipErrorOutOfMemory) ? FRM_ERR_OUT_OF_MEMORY : FRM_ERR_HIP;
+  return fail(ctx, code, "%s failed: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+#define FRM_HIP(ctx, call)                              \
+  do {                                                  \
+    hipError_t e_ = (call);                             \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+  } while (0)
+
+uint32_t num_bands(uint32_t height, uint32_t band_rows) { return (height + band_rows - 1) / band_rows; }
+
+// Rows produced by bands first, first+stride, ... below num_bands (the last band of the
+// frame may be short, but a band buffer always reserves band_rows rows for it).
+uint32_t band_local_rows(uint32_t height, uint32_t band_rows, uint32_t first, uint32_t stride) {
+  uint32_t nb = num_bands(height, band_rows);
+  if (first >= nb) return 0;
+  uint32_t count = (nb - 1 - first) / stride + 1;
+  return count * band_rows;
+}
+
+int ensure_ready(frm_ctx* ctx) {
+  if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->has_params) return fail(ctx, FRM_ERR_NOT_READY, "frm_set_parameters has not been called");
+  return FRM_OK;
+}
+
+KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, uint32_t band_rows,
+                     uint32_t first, uint32_t stride, uint32_t local_rows) {
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  compute_frame_uniforms(ctx->params, ctx->width, ctx->height, ctx->max_steps, &a.f);
+  a.s = ctx->scene;
+  a.g.band_rows = band_rows;
+  a.g.first_band = first;
+  a.g.band_stride = stride;
+  a.g.local_rows = local_rows;
+  a.out = (uint32_t*)dst;
+  a.counters = counters;
+  a.queue = ctx->queue;
+  a.tiles_x = (ctx->width + 7u) / 8u;
+  a.tiles_total = a.tiles_x * ((local_rows + 7u) / 8u);
+  return a;
+}
+
+int launch(frm_ctx* ctx, const KernelArgs& a, hipStream_t s) {
+  if (a.g.local_rows == 0) return FRM_OK;
+  KernelKind kind = (ctx->flags & FRM_FLAG_SIMPLE_KERNEL) ? kKernelSimple : kKernelPersistent;
+  if (kind == kKernelPersistent) FRM_HIP(ctx, hipMemsetAsync(ctx->queue, 0, sizeof(unsigned int), s));
+  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s));
+  return FRM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t frm_abi_version(void) { return FRM_ABI_VERSION; }
+
+const char* frm_last_error(const frm_ctx* ctx) { return ctx ? ctx->error.c_str() : g_error.c_str(); }
+
+int frm_device_count(int32_t* out_count) {
+  if (!out_count) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "out_count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *out_count = 0;
+    return hip_fail(nullptr, e, "hipGetDeviceCount");
+  }
+  *out_count = n;
+  return FRM_OK;
+}
+
+int frm_create(frm_ctx** out_ctx, const frm_config* config) {
+  if (!out_ctx || !config) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "out_ctx/config is NULL");
+  *out_ctx = nullptr;
+  if (config->reserved != 0) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.reserved must be 0");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(nullptr, FRM_ERR_NO_DEVICE, "no HIP device available (%s)", hipGetErrorString(e));
+  if (config->device < 0 || config->device >= n)
+    return fail(nullptr, FRM_ERR_NO_DEVICE, "device %d out of range [0, %d)", config->device, n);
+  frm_ctx* ctx = new (std::nothrow) frm_ctx();
+  if (!ctx) return fail(nullptr, FRM_ERR_OUT_OF_MEMORY, "host allocation failed");
+  ctx->device = config->device;
+  ctx->max_steps = config->max_steps ? config->max_steps : FRM_DEFAULT_MAX_STEPS;
+  ctx->flags = config->flags;
+  int rc = FRM_OK;
+  do {
+    if ((e = hipSetDevice(ctx->device)) != hipSuccess) { rc = hip_fail(ctx, e, "hipSetDevice"); break; }
+    if ((e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, ctx->device)) != hipSuccess) {
+      rc = hip_fail(ctx, e, "hipDeviceGetAttribute"); break;
+    }
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) { rc = hip_fail(ctx, e, "hipStreamCreate"); break; }
+    if ((e = hipEventCreate(&ctx->ev_start)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
+    if ((e = hipEventCreate(&ctx->ev_stop)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
+    if ((e = hipMalloc(&ctx->counters, FRM_NUM_COUNTERS * sizeof(unsigned long long))) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(counters)"); break; }
+    if ((e = hipMalloc(&ctx->queue, 64)) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(queue)"); break; }
+  } while (0);
+  if (rc != FRM_OK) {
+    g_error = ctx->error;
+    frm_destroy(ctx);
+    return rc;
+  }
+  *out_ctx = ctx;
+  return FRM_OK;
+}
+
+int frm_destroy(frm_ctx* ctx) {
+  if (!ctx) return FRM_OK;
+  // Teardown is best effort: statuses are ignored so every resource gets released.
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->fb) (void)hipFree(ctx->fb);
+  if (ctx->counters) (void)hipFree(ctx->counters);
+  if (ctx->queue) (void)hipFree(ctx->queue);
+  if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
+  if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return FRM_OK;
+}
+
+int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
+  if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (width == 0 || height == 0 || width > FRM_MAX_DIMENSION || height > FRM_MAX_DIMENSION)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "frame size %ux%u outside [1, %u]^2", width, height,
+                FRM_MAX_DIMENSION);
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->fb && width == ctx->width && height == ctx->height) return FRM_OK;
+  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->fb) {
+    FRM_HIP(ctx, hipFree(ctx->fb));
+    ctx->fb = nullptr;
+  }
+  ctx->width = ctx->height = 0;
+  FRM_HIP(ctx, hipMalloc(&ctx->fb, (size_t)width * height * 4u));
+  ctx->width = width;
+  ctx->height = height;
+  return FRM_OK;
+}
+
+int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters) {
+  if (!ctx || !parameters) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/parameters is NULL");
+  if (parameters->num_iterations > FRM_MAX_NUM_ITERATIONS)
+    return fail(ctx, FRM_ERR_UNSUPPORTED, "num_iterations %u above FRM_MAX_NUM_ITERATIONS (%u)",
+                parameters->num_iterations, FRM_MAX_NUM_ITERATIONS);
+  ctx->params = *parameters;
+  compute_scene_uniforms(ctx->params, ctx->flags, &ctx->scene);
+  ctx->has_params = true;
+  return FRM_OK;
+}
+
+int frm_render(frm_ctx* ctx, frm_stats* stats) {
+  int rc = ensure_ready(ctx);
+  if (rc) return rc;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  KernelArgs a = make_args(ctx, ctx->fb, ctx->counters, ctx->height, 0, 1, ctx->height);
+  if (stats) {
+    FRM_HIP(ctx, hipMemsetAsync(ctx->counters, 0, FRM_NUM_COUNTERS * sizeof(unsigned long long), ctx->stream));
+    FRM_HIP(ctx, hipEventRecord(ctx->ev_start, ctx->stream));
+  }
+  rc = launch(ctx, a, ctx->stream);
+  if (rc) return rc;
+  if (stats) {
+    FRM_HIP(ctx, hipEventRecord(ctx->ev_stop, ctx->stream));
+    uint64_t host[FRM_NUM_COUNTERS];
+    FRM_HIP(ctx, hipMemcpyAsync(host, ctx->counters, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
+    FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0.0f;
+    FRM_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
+    rc = frm_stats_from_counters(ctx, host, stats);
+    if (rc) return rc;
+    stats->kernel_ms = ms;
+  }
+  return FRM_OK;
+}
+
+int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes) {
+  if (!ctx || !dst) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/dst is NULL");
+  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  size_t need = (size_t)ctx->width * ctx->height * 4u;
+  if (dst_bytes < need)
+    return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, frame needs %zu", dst_bytes, need);
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->fb, need, hipMemcpyDeviceToHost, ctx->stream));
+  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return FRM_OK;
+}
+
+int frm_synchronize(frm_ctx* ctx) {
+  if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return FRM_OK;
+}
+
+int frm_band_rows_for(uint32_t height, uint32_t band_rows, uint32_t first_band, uint32_t band_stride,
+                      uint32_t* out_rows) {
+  if (!out_rows || height == 0 || band_rows == 0 || band_stride == 0)
+    return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "invalid band geometry");
+  *out_rows = band_local_rows(height, band_rows, first_band, band_stride);
+  return FRM_OK;
+}
+
+int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t band_rows,
+                     uint32_t first_band, uint32_t band_stride, void* stream, uint64_t* dev_counters) {
+  int rc = ensure_ready(ctx);
+  if (rc) return rc;
+  if (!dev_dst || band_rows == 0 || band_stride == 0)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "invalid dst or band geometry");
+  uint32_t rows = band_local_rows(ctx->height, band_rows, first_band, band_stride);
+  size_t need = (size_t)rows * ctx->width * 4u;
+  if (dst_bytes < need)
+    return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, bands need %zu", dst_bytes, need);
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  unsigned long long* counters = dev_counters ? (unsigned long long*)dev_counters : ctx->counters;
+  KernelArgs a = make_args(ctx, dev_dst, counters, band_rows, first_band, band_stride, rows);
+  return launch(ctx, a, s);
+}
+
+int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride_bytes, uint8_t* dev_dst,
+                        size_t dst_bytes, uint32_t band_rows, uint32_t ranks, void* stream) {
+  if (!ctx || !dev_src || !dev_dst || band_rows == 0 || ranks == 0)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "invalid unshuffle arguments");
+  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  size_t need = (size_t)ctx->width * ctx->height * 4u;
+  if (dst_bytes < need)
+    return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, frame needs %zu", dst_bytes, need);
+  uint32_t rows = band_local_rows(ctx->height, band_rows, 0, ranks);
+  if (rank_stride_bytes < (size_t)rows * ctx->width * 4u)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "rank stride %zu below one rank's bands", rank_stride_bytes);
+  if (rank_stride_bytes % 4u)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "rank stride must be a multiple of 4");
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FRM_HIP(ctx, launch_unshuffle(dev_src, rank_stride_bytes, dev_dst, ctx->width, ctx->height, band_rows,
+                                ranks, s));
+  return FRM_OK;
+}
+
+int frm_stats_from_counters(const frm_ctx* ctx, const uint64_t* c, frm_stats* out) {
+  if (!ctx || !c || !out) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
+  memset(out, 0, sizeof(*out));
+  out->pixels = c[kCntPixels];
+  out->hit_pixels = c[kCntHits];
+  out->primary_steps = c[kCntPrimary];
+  out->shadow_steps = c[kCntShadow];
+  out->normal_evals = c[kCntNormal];
+  out->fractal_bodies = c[kCntBodies];
+  out->fractal_bailouts = c[kCntBailouts];
+  out->march_steps = c[kCntPrimary] + c[kCntShadow];
+  out->wom_ops = wom_ops(ctx->scene, c);
+  return FRM_OK;
+}
+
+int frm_eval_scene(frm_ctx* ctx, const float* points, uint32_t n, float* out_distance, float* out_color) {
+  if (!ctx || !points || !out_distance || !out_color)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (!ctx->has_params) return fail(ctx, FRM_ERR_NOT_READY, "frm_set_parameters has not been called");
+  if (n == 0) return FRM_OK;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  float* d = nullptr;
+  FRM_HIP(ctx, hipMalloc(&d, (size_t)n * 7 * sizeof(float)));
+  float *pts = d, *dist = d + 3 * (size_t)n, *col = d + 4 * (size_t)n;
+  hipError_t e = hipMemcpyAsync(pts, points, (size_t)n * 12, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = launch_eval_scene(ctx->scene, pts, n, dist, col, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_distance, dist, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_color, col, (size_t)n * 12, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "frm_eval_scene");
+  return FRM_OK;
+}
+
+int frm_eval_math(frm_ctx* ctx, int32_t fn, const float* a, const float* b, uint32_t n, float* out) {
+  if (!ctx || !a || !out || fn < 0 || fn > FRM_MATH_DIV) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad argument");
+  if (n == 0) return FRM_OK;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  float* d = nullptr;
+  FRM_HIP(ctx, hipMalloc(&d, (size_t)n * 3 * sizeof(float)));
+  float *da = d, *db = b ? d + n : nullptr, *dout = d + 2 * (size_t)n;
+  hipError_t e = hipMemcpyAsync(da, a, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess && b) e = hipMemcpyAsync(db, b, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = launch_eval_math(fn, da, db, n, dout, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "frm_eval_math");
+  return FRM_OK;
+}
+
+}  // extern "C"

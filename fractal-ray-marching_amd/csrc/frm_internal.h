@@ -1,0 +1,34 @@
+// frm_internal.h — declarations shared by libfrm's translation units (not installed).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "frm_uniforms.h"
+
+namespace frm {
+// Row-band geometry of one launch: local row lr lives in band (lr / band_rows) of this
+// launch; that band is global band first_band + (lr / band_rows) * band_stride.
+struct BandGeometry {
+  uint32_t band_rows, first_band, band_stride, local_rows;
+};
+
+struct KernelArgs {
+  FrameUniforms f;
+  SceneUniforms s;
+  BandGeometry g;
+  uint32_t* out;                  // packed RGBA8 words, local row-major, pitch = width
+  unsigned long long* counters;   // FRM_NUM_COUNTERS, accumulated
+  unsigned int* queue;            // persistent kernel: work-queue head (zeroed per launch)
+  uint32_t tiles_x, tiles_total;  // persistent kernel: 8x8 pixel tiles of the launch
+};
+
+// frm_kernels.hip
+enum KernelKind : uint32_t { kKernelPersistent = 0, kKernelSimple = 1 };
+hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream);
+hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,
+                            uint32_t height, uint32_t band_rows, uint32_t ranks,
+                            hipStream_t stream);
+hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
+                             hipStream_t stream);
+hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, float* out, hipStream_t stream);
+
+}  // namespace frm

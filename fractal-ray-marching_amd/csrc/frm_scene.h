@@ -1,0 +1,357 @@
+// frm_scene.h — per-frame uniforms and the per-pixel hot path of src/fragment.wgsl
+// (scene dispatch 18-78, distance estimators 118-271, march 273-304, normal 306-313,
+// camera 315-325, shading 327-349) restated for a gfx950 compute kernel.
+//
+// Design: everything that depends only on Parameters (fractal family, animated
+// constants, plane normals, camera rows) is hoisted to the host once per frame
+// (SceneUniforms / FrameUniforms, filled by frm_host.cpp) and reaches the kernel by
+// value in the kernarg segment (scalar registers). The device code is templated on the
+// fractal family so the scene switch (fragment.wgsl:19) costs nothing per step.
+#pragma once
+#include "frm_math.h"
+
+// FRM_ASSUME(c): tell the optimizer c holds (see "ITERS" below).
+#if defined(__clang__)
+#define FRM_ASSUME(c) __builtin_assume(c)
+#else
+#define FRM_ASSUME(c) \
+  do {                \
+    if (!(c)) __builtin_unreachable(); \
+  } while (0)
+#endif
+
+namespace frm {
+
+// ITERS template flag: false <=> num_iterations == 0. The fractal loops of every family
+// are compiled twice: without a loop (ITERS = false) and with the trip count asserted
+// to be >= 1 (ITERS = true), so no device code ever evaluates the uniform guard
+// "num_iterations > 0" inside the divergent march loop. ROCm 7.2's AMDGPU backend
+// miscompiles that guard (it is rematerialised as a lane mask under the loop's exec
+// mask and reused after the loop with a different exec mask), which re-entered the
+// fold loop for lanes that had left the march early (DESIGN.md §"Compiler workaround").
+template <bool ITERS>
+FRM_HD uint32_t iterations(uint32_t n) {
+  if (!ITERS) return 0u;
+  FRM_ASSUME(n >= 1u && n <= 4096u);
+  return n;
+}
+
+enum Family : uint32_t {
+  kMenger = 0,      // scenes 0-14          fragment.wgsl:202-211
+  kSierpinski = 1,  // scene 15             fragment.wgsl:164-188
+  kKoch = 2,        // scenes 16-17         fragment.wgsl:213-238
+  kMandelbulb = 3,  // scene 18             fragment.wgsl:240-271
+  kSphere = 4,      // build extension (BASELINE config C1), not in the reference
+};
+
+// Constants of fragment.wgsl:1-16 and 92-94 (abstract floats rounded once to f32).
+constexpr float kMaxTotalDistance = 1000.0f;          // :2
+constexpr float kMinDistance = 4.99999987376214e-07f; // :3  f32(5e-7)
+constexpr float kInfinity = 1.00000002004087734e+20f; // :94 f32(pow(10,20))
+constexpr float kCameraDirectionZ = 0x1.fe04c8p-1f;  // :329 f32(1/atan(pi/2)) = 0.99613023
+constexpr float kToSunX = 0.666666686534881592f;      // :337 normalize(-SUN_DIRECTION)
+constexpr float kToSunY = 0.333333343267440796f;
+constexpr float kToSunZ = -0.666666686534881592f;
+constexpr float kShadowFactor = 0.699999988079071045f;   // :11 f32(0.7)
+constexpr float kShadowSharpness = 32.0f;               // :12
+constexpr float kSpecularFactor = 0.150000005960464478f; // :13 f32(0.15)
+constexpr float kSpecularSharpness = 16.0f;             // :14
+constexpr float kAOFactor = 0.200000002980232239f;      // :15 f32(0.2)
+constexpr float kAOSharpness = 100.0f;                  // :16
+
+struct Plane {
+  v3 anchor, normal;
+};
+
+struct SceneUniforms {
+  uint32_t family;
+  uint32_t n;            // parameters.num_iterations
+  // Menger (cross_size, scale_factor), fragment.wgsl:21-63
+  float menger_cross, menger_factor;
+  // Mandelbulb power = animate_between(4, 9), bailout 100, fragment.wgsl:75
+  float mb_power, mb_power_m1, mb_bailout;
+  // Sierpinski: TOP.y, HEIGHT*BASE_SCALE_FACTOR*0.5, a/b/c - TOP, fold normals
+  float sp_top_y, sp_yoff;
+  v3 sp_top[3];
+  v3 sp_normal[3];
+  // Koch: mirror normals, OFFSET, final scale_factor
+  v3 koch_n1, koch_n2;
+  float koch_offset, koch_scale;
+  // tetrahedron() planes (Sierpinski: TOP,a,b,c; Koch: TOP,LEFT,RIGHT,BACK)
+  Plane tet[4];
+};
+
+struct FrameUniforms {
+  float row[3][4];    // camera_matrix columns 0..2 (= rows of the cgmath matrix)
+  v3 origin;          // transform_position(Position(0)), fragment.wgsl:331
+  float aspect_x, aspect_y;
+  uint32_t width, height;
+  uint32_t max_steps;
+  float max_steps_f;  // Scalar(MAX_ITERATIONS)
+};
+
+// ---- distance estimators -----------------------------------------------------
+// Mandelbulb work counters (data dependent); the other families' work is a fixed
+// function of num_iterations.
+struct DeCount {
+  uint32_t bodies;
+  uint32_t bailouts;
+};
+
+// mirror(position, anchor, normal), fragment.wgsl:159-162
+FRM_HD v3 mirror(v3 p, v3 anchor, v3 n) {
+  float d = dot(p - anchor, n);
+  return fma3(fabsf(d) - d, n, p);
+}
+// mirror about a plane through the origin: position - Position(0) == position exactly.
+FRM_HD v3 mirror0(v3 p, v3 n) {
+  float d = dot(p, n);
+  return fma3(fabsf(d) - d, n, p);
+}
+// tetrahedron(...), fragment.wgsl:151-157 (planes precomputed on the host)
+FRM_HD float tetrahedron(const SceneUniforms& u, v3 p) {
+  float h0 = dot(p - u.tet[0].anchor, u.tet[0].normal);
+  float h1 = dot(p - u.tet[1].anchor, u.tet[1].normal);
+  float h2 = dot(p - u.tet[2].anchor, u.tet[2].normal);
+  float h3 = dot(p - u.tet[3].anchor, u.tet[3].normal);
+  return max_(max_(max_(h0, h1), h2), h3);
+}
+
+// menger_sponge(position, cross_size, scale_factor), fragment.wgsl:202-211, with
+// box (138-141), repeat (190-192), cross_inside (194-200).
+template <bool ITERS>
+FRM_HD float de_menger(const SceneUniforms& u, v3 p) {
+  const uint32_t n = iterations<ITERS>(u.n);
+  v3 q = mk(fabsf(p.x) - 0.5f, fabsf(p.y) - 0.5f, fabsf(p.z) - 0.5f);
+  float d = length(max3s(q, 0.0f)) + min_(max_(max_(q.x, q.y), q.z), 0.0f);
+  float scale = 1.0f;
+  for (uint32_t i = 0; i < n; ++i) {
+    v3 r = p * scale;
+    v3 c = mk(fract_(r.x + 0.5f) - 0.5f, fract_(r.y + 0.5f) - 0.5f, fract_(r.z + 0.5f) - 0.5f);
+    v3 a = abs3(c);
+    float cx = max_(a.y, a.z), cy = max_(a.z, a.x), cz = max_(a.x, a.y);
+    float ci = min_(min_(cx, cy), cz) - u.menger_cross;
+    d = max_(d, (-ci) / scale);
+    scale = scale * u.menger_factor;
+  }
+  return d;
+}
+
+// sierpinski_tetrahedron(position), fragment.wgsl:164-188. The loop runs i = N-1 .. 0
+// (num_iterations <= FRM_MAX_NUM_ITERATIONS < 2^31, so i32(N) - 1 >= -1).
+template <bool ITERS>
+FRM_HD float de_sierpinski(const SceneUniforms& u, v3 p) {
+  const uint32_t n = iterations<ITERS>(u.n);
+  v3 q = mk(p.x, p.y + u.sp_yoff, p.z);
+  v3 top = mk(0.0f, u.sp_top_y, 0.0f);
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t i = n - 1u - j;
+    float dist = (float)(int32_t)(1u << (i & 31u));  // Scalar(1 << u32(i)), i32
+    q = mirror(q, fma3(dist, u.sp_top[0], top), u.sp_normal[0]);
+    q = mirror(q, fma3(dist, u.sp_top[1], top), u.sp_normal[1]);
+    q = mirror(q, fma3(dist, u.sp_top[2], top), u.sp_normal[2]);
+  }
+  return tetrahedron(u, q);
+}
+
+// koch3D(position, normal_z), fragment.wgsl:213-238.
+template <bool ITERS>
+FRM_HD float de_koch(const SceneUniforms& u, v3 p) {
+  const uint32_t n = iterations<ITERS>(u.n);
+  v3 q = p * 2.0f;
+  for (uint32_t i = 0; i < n; ++i) {
+    q = q * 1.5f;
+    q = mk(q.y, q.x, q.z);
+    q = mirror0(q, u.koch_n1);
+    q = mirror0(q, u.koch_n2);
+    q.z = q.z - u.koch_offset;
+  }
+  q.y = fabsf(q.y);
+  return tetrahedron(u, q) / u.koch_scale;
+}
+
+// mandelbulb(position, power, bailout), fragment.wgsl:240-271. N+1 bodies; pow(r, y)
+// is exp2(y*log2(r)) (frm semantics), so log2(r) is shared by both pows.
+template <bool ITERS>
+FRM_HD float de_mandelbulb(const SceneUniforms& u, v3 p, DeCount& cnt) {
+  const uint32_t n = iterations<ITERS>(u.n);
+  v3 z = p;
+  float dr = 1.0f;
+  float r = 0.0f;
+  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+  for (uint32_t i = 0;; ++i) {
+    r = length(z);
+    if (r > u.mb_bailout) {
+      cnt.bailouts++;
+      break;
+    }
+    float theta = acos_(z.z / r);
+    float phi = atan2_(z.y, z.x);
+    float l2 = log2_(r);
+    dr = fma_(exp2_(Pm1 * l2) * P, dr, 1.0f);
+    float er = exp2_(P * l2);
+    float st, ct, sp, cp;
+    sincos_(theta * P, &st, &ct);
+    sincos_(phi * P, &sp, &cp);
+    z = mk(fma_(er, st * cp, p.x), fma_(er, sp * st, p.y), fma_(er, ct, p.z));
+    cnt.bodies++;
+    if (i == n) break;
+  }
+  return ((0.5f * log_(r)) * r) / dr;
+}
+
+FRM_HD float de_sphere(v3 p) { return length(p) - 0.5f; }
+
+template <uint32_t FAM, bool ITERS>
+FRM_HD float scene_de(const SceneUniforms& u, v3 p, DeCount& cnt) {
+  if constexpr (FAM == kMenger) return de_menger<ITERS>(u, p);
+  else if constexpr (FAM == kSierpinski) return de_sierpinski<ITERS>(u, p);
+  else if constexpr (FAM == kKoch) return de_koch<ITERS>(u, p);
+  else if constexpr (FAM == kMandelbulb) return de_mandelbulb<ITERS>(u, p, cnt);
+  else return de_sphere(p);
+}
+
+// Object colour at a hit: colorize(position), or colorize(1.5*position) for Sierpinski.
+template <uint32_t FAM>
+FRM_HD v3 scene_color(v3 p) {
+  if constexpr (FAM == kSierpinski) return colorize(p * 1.5f);
+  else return colorize(p);
+}
+
+// ---- camera / ray generation ----------------------------------------------------
+// Pixel centre of the full-screen quad (vertex.wgsl:6-17, WebGPU y-up NDC, row 0 = top).
+FRM_HD float screen_x(uint32_t x, uint32_t w) { return (float)(2u * x + 1u) / (float)w - 1.0f; }
+FRM_HD float screen_y(uint32_t y, uint32_t h) { return 1.0f - (float)(2u * y + 1u) / (float)h; }
+
+// (vec4(d, 0) * camera_matrix).xyz, fragment.wgsl:315-325; dot4 = fma chain.
+FRM_HD v3 camera_ray(const FrameUniforms& f, uint32_t x, uint32_t y) {
+  float sx = screen_x(x, f.width), sy = screen_y(y, f.height);
+  v3 d = normalize(mk(sx * f.aspect_x, sy * f.aspect_y, kCameraDirectionZ));
+  v3 o;
+  o.x = fma_(0.0f, f.row[0][3], fma_(d.z, f.row[0][2], fma_(d.y, f.row[0][1], d.x * f.row[0][0])));
+  o.y = fma_(0.0f, f.row[1][3], fma_(d.z, f.row[1][2], fma_(d.y, f.row[1][1], d.x * f.row[1][0])));
+  o.z = fma_(0.0f, f.row[2][3], fma_(d.z, f.row[2][2], fma_(d.y, f.row[2][1], d.x * f.row[2][0])));
+  return o;
+}
+
+// ---- shading helpers (fragment.wgsl:336-346) ----------------------------------------
+FRM_HD v3 to_sun() { return mk(kToSunX, kToSunY, kToSunZ); }
+
+// Normal from the four tetrahedral taps d0..d3 (k.xyy, k.yyx, k.yxy, k.xxx),
+// fragment.wgsl:306-313: sum left to right, then normalize.
+FRM_HD v3 normal_from_taps(float d0, float d1, float d2, float d3) {
+  v3 s = mk(((d0 - d1) - d2) + d3, ((-d0 - d1) + d2) + d3, ((-d0 + d1) - d2) + d3);
+  return normalize(s);
+}
+FRM_HD v3 normal_tap_pos(v3 p, int k) {
+  const float e = kMinDistance;
+  switch (k) {
+    case 0: return mk(p.x + e, p.y + -e, p.z + -e);
+    case 1: return mk(p.x + -e, p.y + -e, p.z + e);
+    case 2: return mk(p.x + -e, p.y + e, p.z + -e);
+    default: return mk(p.x + e, p.y + e, p.z + e);
+  }
+}
+
+// Final colour of a hit pixel given the primary colour, camera direction, normal,
+// primary step count and the shadow march result. fragment.wgsl:337-346.
+FRM_HD v3 shade_hit(const FrameUniforms& f, v3 color, v3 dir, v3 n, uint32_t steps,
+                    float sun_distance, float sun_closeness) {
+  v3 halfway = normalize(-dir + to_sun());
+  float specular = pow_(max_(dot(halfway, n), 0.0f), kSpecularSharpness);
+  float ao = pow_(1.0f - (float)steps / f.max_steps_f, kAOSharpness);
+  color = color * mix_(kAOFactor, 1.0f, ao);
+  float shadow = ((sun_distance < 0.0f ? 1.0f : 0.0f) * kShadowSharpness) * sun_closeness;
+  color = color * mix_(kShadowFactor, 1.0f, clamp_(shadow, 0.0f, 1.0f));
+  float add = ((kSpecularFactor * shadow) * specular) * 1.0f;
+  return mk(color.x + add, color.y + add, color.z + add);
+}
+// Shadow-ray origin: object_position + object_normal * 2 * MIN_DISTANCE (contracted).
+FRM_HD v3 shadow_origin(v3 pos, v3 n) {
+  return mk(fma_(n.x * 2.0f, kMinDistance, pos.x), fma_(n.y * 2.0f, kMinDistance, pos.y),
+            fma_(n.z * 2.0f, kMinDistance, pos.z));
+}
+// start_position + total_distance * direction (contracted), fragment.wgsl:290.
+FRM_HD v3 ray_at(v3 o, float t, v3 d) { return mk(fma_(t, d.x, o.x), fma_(t, d.y, o.y), fma_(t, d.z, o.z)); }
+
+// ---- march + fragment_main ------------------------------------------------------------
+struct MarchState {
+  v3 pos;
+  float total;
+  float closeness;
+  uint32_t steps;
+  bool hit;
+};
+
+// march(start_position, direction), fragment.wgsl:281-304. `evals` counts scene()
+// calls in the loop (= steps, +1 on a hit). Closeness is only needed by the shadow ray.
+template <uint32_t FAM, bool ITERS, bool CLOSENESS>
+FRM_HD MarchState march(const SceneUniforms& su, uint32_t max_steps, v3 o, v3 d, DeCount& cnt,
+                        uint32_t& evals) {
+  MarchState m;
+  m.pos = o;
+  m.hit = false;
+  float total = 0.0f, closeness = kInfinity;
+  uint32_t it = 0;
+  for (; it < max_steps && total < kMaxTotalDistance; ++it) {
+    v3 p = ray_at(o, total, d);
+    float de = scene_de<FAM, ITERS>(su, p, cnt);
+    evals++;
+    if (CLOSENESS) closeness = min_(closeness, de / total);
+    if (de <= kMinDistance) {
+      m.hit = true;
+      m.pos = p;
+      break;
+    }
+    total = total + de;
+  }
+  m.total = total;
+  m.closeness = closeness;
+  m.steps = it;
+  return m;
+}
+
+struct PixelCount {
+  uint32_t hit, primary, shadow, normal;
+  DeCount de;
+};
+
+// fragment_main(screen_position) for pixel (x, y): the linear colour. fragment.wgsl:327-349.
+template <uint32_t FAM, bool ITERS>
+FRM_HD v3 shade_pixel(const FrameUniforms& f, const SceneUniforms& su, uint32_t x, uint32_t y,
+                      PixelCount& pc) {
+  v3 dir = camera_ray(f, x, y);
+  MarchState m = march<FAM, ITERS, false>(su, f.max_steps, f.origin, dir, pc.de, pc.primary);
+  v3 color = mk(0.0f, 0.0f, 0.0f);
+  if (m.hit) {  // object_result.distance >= 0
+    pc.hit = 1;
+    color = scene_color<FAM>(m.pos);
+    float d0 = scene_de<FAM, ITERS>(su, normal_tap_pos(m.pos, 0), pc.de);
+    float d1 = scene_de<FAM, ITERS>(su, normal_tap_pos(m.pos, 1), pc.de);
+    float d2 = scene_de<FAM, ITERS>(su, normal_tap_pos(m.pos, 2), pc.de);
+    float d3 = scene_de<FAM, ITERS>(su, normal_tap_pos(m.pos, 3), pc.de);
+    pc.normal += 4;
+    v3 n = normal_from_taps(d0, d1, d2, d3);
+    MarchState sun = march<FAM, ITERS, true>(su, f.max_steps, shadow_origin(m.pos, n), to_sun(), pc.de, pc.shadow);
+    color = shade_hit(f, color, dir, n, m.steps, sun.hit ? sun.total : -kInfinity, sun.closeness);
+  }
+  return color;
+}
+
+// Linear colour -> sRGB 8-bit code: the number of thresholds T[1..255] that c reaches.
+// T[k] is the smallest f32 whose exact sRGB encoding rounds to >= k (frm_srgb_table.h),
+// so this equals round(255 * srgb(clamp(c, 0, 1))) exactly; NaN -> 0 (UNORM rule).
+FRM_HD uint32_t encode_srgb(float c, const float* table) {
+  uint32_t i = 0;
+#pragma unroll
+  for (uint32_t step = 128; step >= 1; step >>= 1)
+    if (c >= table[i + step]) i += step;
+  return i;
+}
+
+FRM_HD uint32_t pack_rgba(v3 c, const float* table) {
+  return encode_srgb(c.x, table) | (encode_srgb(c.y, table) << 8) | (encode_srgb(c.z, table) << 16) |
+         (255u << 24);
+}
+
+}  // namespace frm

@@ -1,0 +1,139 @@
+"""ctypes binding of libfrm.so (include/frm.h).
+
+The library is built in-tree by `make -C fractal-ray-marching_amd` (or
+__graft_entry__.build()) into fractal-ray-marching_amd/lib/libfrm.so. There is no
+fallback: if the library is missing, importing the renderer raises.
+"""
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfrm.so")
+
+FRM_OK = 0
+FRM_ERR_INVALID_ARGUMENT = 1
+FRM_ERR_NO_DEVICE = 2
+FRM_ERR_HIP = 3
+FRM_ERR_OUT_OF_MEMORY = 4
+FRM_ERR_NOT_READY = 5
+FRM_ERR_BUFFER_TOO_SMALL = 6
+FRM_ERR_UNSUPPORTED = 7
+
+FRM_NUM_SCENES = 19
+FRM_DEFAULT_MAX_STEPS = 5000
+FRM_MAX_NUM_ITERATIONS = 4096
+FRM_NUM_COUNTERS = 8
+FRM_FLAG_SCENE_SPHERE = 0x1
+FRM_FLAG_SIMPLE_KERNEL = 0x2
+
+
+class FrmParameters(ctypes.Structure):
+    """src/parameters.rs:6-15, byte for byte (96 bytes)."""
+
+    _fields_ = [
+        ("camera_matrix", ctypes.c_float * 16),
+        ("aspect_scale", ctypes.c_float * 2),
+        ("time", ctypes.c_float),
+        ("num_iterations", ctypes.c_uint32),
+        ("scene_index", ctypes.c_uint32),
+        ("padding", ctypes.c_uint8 * 12),
+    ]
+
+
+class FrmConfig(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("max_steps", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class FrmStats(ctypes.Structure):
+    _fields_ = [
+        ("pixels", ctypes.c_uint64),
+        ("hit_pixels", ctypes.c_uint64),
+        ("primary_steps", ctypes.c_uint64),
+        ("shadow_steps", ctypes.c_uint64),
+        ("normal_evals", ctypes.c_uint64),
+        ("fractal_bodies", ctypes.c_uint64),
+        ("fractal_bailouts", ctypes.c_uint64),
+        ("march_steps", ctypes.c_uint64),
+        ("wom_ops", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+assert ctypes.sizeof(FrmParameters) == 96
+
+_P = ctypes.POINTER
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+# (name, restype, argtypes) for every entry point declared in include/frm.h
+SIGNATURES = [
+    ("frm_abi_version", ctypes.c_uint32, []),
+    ("frm_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("frm_device_count", ctypes.c_int, [_P(ctypes.c_int32)]),
+    ("frm_create", ctypes.c_int, [_P(ctypes.c_void_p), _P(FrmConfig)]),
+    ("frm_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("frm_resize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]),
+    ("frm_set_parameters", ctypes.c_int, [ctypes.c_void_p, _P(FrmParameters)]),
+    ("frm_render", ctypes.c_int, [ctypes.c_void_p, _P(FrmStats)]),
+    ("frm_read_frame", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("frm_synchronize", ctypes.c_int, [ctypes.c_void_p]),
+    ("frm_band_rows_for", ctypes.c_int,
+     [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint32)]),
+    ("frm_render_bands", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("frm_unshuffle_bands", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    ("frm_stats_from_counters", ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_uint64), _P(FrmStats)]),
+    ("frm_eval_scene", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("frm_eval_math", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("frm_parameters_default", None, [_P(FrmParameters)]),
+    ("frm_parameters_update_aspect", None, [_P(FrmParameters), ctypes.c_uint32, ctypes.c_uint32]),
+    ("frm_parameters_update_time", None, [_P(FrmParameters), ctypes.c_float]),
+    ("frm_parameters_update_num_iterations", None, [_P(FrmParameters), ctypes.c_int32]),
+    ("frm_parameters_update_scene_index", None, [_P(FrmParameters), ctypes.c_int32]),
+    ("frm_parameters_update_camera", None,
+     [_P(FrmParameters), _P(ctypes.c_float), ctypes.c_float, ctypes.c_float]),
+]
+
+_lib = None
+
+
+class FrmError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__(f"libfrm error {code}: {message}")
+        self.code = code
+
+
+def load():
+    """Load libfrm.so (raises OSError with a build hint if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} not found: build it with `make -C {PKG_ROOT}` "
+                      "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, restype, argtypes in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    _lib = lib
+    return lib
+
+
+def check(rc, ctx=None):
+    if rc != FRM_OK:
+        msg = load().frm_last_error(ctx)
+        raise FrmError(rc, msg.decode() if msg else "")
+    return rc

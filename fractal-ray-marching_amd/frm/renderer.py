@@ -1,0 +1,110 @@
+"""Renderer: the Python host's view of libfrm, mirroring the reference's `Graphics`
+API (src/graphics.rs): init -> resize -> update_parameters_buffer -> render ->
+(read_frame replaces the blit+present). Errors raise FrmError; nothing falls back to
+the CPU."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+class Renderer:
+    def __init__(self, device=0, max_steps=0, flags=0):
+        lib = _lib.load()
+        self._lib = lib
+        self.ctx = ctypes.c_void_p()
+        cfg = _lib.FrmConfig(device, max_steps, flags, 0)
+        _lib.check(lib.frm_create(ctypes.byref(self.ctx), ctypes.byref(cfg)))
+        self.device = device
+        self.width = self.height = 0
+
+    def close(self):
+        if self.ctx:
+            self._lib.frm_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        return _lib.check(rc, self.ctx)
+
+    # graphics.rs:54-57 (render texture size) — arbitrary W x H here
+    def resize(self, width, height):
+        self._check(self._lib.frm_resize(self.ctx, width, height))
+        self.width, self.height = width, height
+
+    # graphics.rs:59-61
+    def update_parameters_buffer(self, parameters):
+        raw = parameters.raw if hasattr(parameters, "raw") else parameters
+        self._check(self._lib.frm_set_parameters(self.ctx, ctypes.byref(raw)))
+
+    # graphics.rs:91-110 (one frame); returns frm_stats as a dict when stats=True
+    def render(self, stats=True):
+        if not stats:
+            self._check(self._lib.frm_render(self.ctx, None))
+            return None
+        st = _lib.FrmStats()
+        self._check(self._lib.frm_render(self.ctx, ctypes.byref(st)))
+        return st.as_dict()
+
+    def read_frame(self):
+        buf = np.empty((self.height, self.width, 4), dtype=np.uint8)
+        self._check(self._lib.frm_read_frame(self.ctx, buf.ctypes.data, buf.nbytes))
+        return buf
+
+    def synchronize(self):
+        self._check(self._lib.frm_synchronize(self.ctx))
+
+    # multi-GPU row tiling (device pointers, e.g. torch tensors' data_ptr())
+    def render_bands(self, dev_ptr, nbytes, band_rows, first_band, band_stride, stream=0,
+                     dev_counters=0):
+        self._check(self._lib.frm_render_bands(self.ctx, dev_ptr, nbytes, band_rows, first_band,
+                                               band_stride, stream or None, dev_counters or None))
+
+    def unshuffle_bands(self, src_ptr, rank_stride, dst_ptr, dst_bytes, band_rows, ranks, stream=0):
+        self._check(self._lib.frm_unshuffle_bands(self.ctx, src_ptr, rank_stride, dst_ptr, dst_bytes,
+                                                  band_rows, ranks, stream or None))
+
+    # diagnostics: scene() and builtins evaluated on the GPU
+    MATH_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "log": 4, "log2": 5, "exp2": 6,
+               "pow": 7, "sqrt": 8, "div": 9}
+
+    def eval_scene(self, points):
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        d = np.zeros(len(pts), np.float32)
+        col = np.zeros((len(pts), 3), np.float32)
+        self._check(self._lib.frm_eval_scene(self.ctx, pts.ctypes.data, len(pts), d.ctypes.data,
+                                             col.ctypes.data))
+        return d, col
+
+    def eval_math(self, name, a, b=None):
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        bb = None if b is None else np.ascontiguousarray(np.broadcast_to(b, a.shape), dtype=np.float32)
+        out = np.zeros_like(a)
+        self._check(self._lib.frm_eval_math(self.ctx, self.MATH_FN[name], a.ctypes.data,
+                                            None if bb is None else bb.ctypes.data, a.size,
+                                            out.ctypes.data))
+        return out
+
+    def stats_from_counters(self, counters):
+        arr = (ctypes.c_uint64 * _lib.FRM_NUM_COUNTERS)(*[int(c) for c in counters])
+        st = _lib.FrmStats()
+        self._check(self._lib.frm_stats_from_counters(self.ctx, arr, ctypes.byref(st)))
+        return st.as_dict()
+
+
+def device_count():
+    n = ctypes.c_int32(0)
+    rc = _lib.load().frm_device_count(ctypes.byref(n))
+    return n.value if rc == _lib.FRM_OK else 0

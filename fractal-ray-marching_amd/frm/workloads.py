@@ -1,0 +1,57 @@
+"""Fixed benchmark poses and the BASELINE.json configurations."""
+import math
+from dataclasses import dataclass
+
+from .parameters import Camera, Parameters
+
+# asin(0.6)/0.2: animate_between(4, 9) == 8.0 exactly in f32 -> Mandelbulb power 8.
+POWER8_TIME = 3.2175055
+
+POSES = {
+    # name: (position, yaw, pitch)
+    "P0": ((0.0, 0.0, -2.5), 0.0, 0.0),
+    "P1": ((0.0, 0.0, -1.6), 0.0, 0.0),
+    # yaw-lock "inwards" + pitch-lock (camera.rs:129-147) at (1.5, 0.9, -1.5)
+    "P2": ((1.5, 0.9, -1.5), -math.pi / 4, 0.4),
+}
+
+
+@dataclass(frozen=True)
+class Workload:
+    name: str
+    width: int
+    height: int
+    scene: int
+    iters: int
+    max_steps: int
+    time: float
+    sphere: bool = False
+    note: str = ""
+
+
+WORKLOADS = {
+    "C1": Workload("C1-sphere-256", 256, 256, 0, 0, 64, 0.0, sphere=True,
+                   note="256x256 single-sphere SDF (build extension), 64 steps"),
+    "C2": Workload("C2-mandelbulb-1080p", 1920, 1080, 18, 12, 256, POWER8_TIME,
+                   note="1920x1080 Mandelbulb power 8, 12 iters, 256 steps"),
+    "C3": Workload("C3-menger-4k", 3840, 2160, 0, 8, 512, 0.0,
+                   note="3840x2160 Menger sponge, 8 iters, 512 steps"),
+    "C4": Workload("C4-mandelbulb-8k", 7680, 4320, 18, 16, 512, POWER8_TIME,
+                   note="7680x4320 Mandelbulb, 16 iters, 512 steps"),
+    "C5": Workload("C5-mandelbulb-16k", 16384, 16384, 18, 20, 1024, POWER8_TIME,
+                   note="16384x16384 animated Mandelbulb, 20 iters, 1024 steps"),
+    "HEADLINE": Workload("headline-mandelbulb-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
+                         note="3840x2160 Mandelbulb power 8, 12 iters, 256 steps"),
+}
+
+
+def make_parameters(w, pose="P1", time=None, width=None, height=None):
+    """Parameters for workload `w` at a fixed pose (aspect from the frame size)."""
+    pos, yaw, pitch = POSES[pose]
+    p = Parameters()
+    p.update_aspect(width or w.width, height or w.height)
+    p.update_camera(Camera(pos, yaw, pitch))
+    p.time = w.time if time is None else time
+    p.num_iterations = w.iters
+    p.scene_index = w.scene
+    return p

@@ -1,0 +1,191 @@
+/*
+ * frm.h — C ABI of the MI355X-native offscreen fractal ray-marcher (libfrm.so).
+ *
+ * This is the drop-in boundary that replaces the reference's wgpu graphics layer
+ * (MariusDoe/fractal-ray-marching: src/graphics.rs, src/persistent_graphics.rs,
+ * src/reloadable_graphics.rs, src/blit_graphics.rs) for the one hot path the
+ * reference has: the per-pixel sphere tracer `fragment_main` in src/fragment.wgsl:327-349.
+ * The caller keeps the reference's own `Parameters` uniform (src/parameters.rs:6-15)
+ * byte for byte; `frm_parameters` below is that struct.
+ *
+ * Conventions
+ *   - Every entry point returns an `int` status (FRM_OK = 0). Nothing aborts, throws
+ *     or panics across the ABI. The message of the last failure on a context is
+ *     available from frm_last_error(); failures before a context exists are available
+ *     from frm_last_error(NULL) (thread-local).
+ *   - A context drives one GPU and is not thread-safe (one context per host thread),
+ *     mirroring the reference's single winit event-loop thread (src/app.rs).
+ *   - Rendering is stream-ordered. frm_render() with a NULL stats pointer is
+ *     asynchronous; frm_read_frame()/frm_synchronize() wait for it.
+ *   - Plain pointers and sizes only; `void* stream` is a hipStream_t (NULL = the
+ *     context's own stream).
+ */
+#ifndef FRM_H
+#define FRM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRM_ABI_VERSION 1u
+
+/* ---- status codes -------------------------------------------------------- */
+enum {
+  FRM_OK = 0,
+  FRM_ERR_INVALID_ARGUMENT = 1, /* NULL pointer, zero size, out-of-range value       */
+  FRM_ERR_NO_DEVICE = 2,        /* no HIP device / device index out of range          */
+  FRM_ERR_HIP = 3,              /* a HIP runtime call failed (message has the name)   */
+  FRM_ERR_OUT_OF_MEMORY = 4,    /* device allocation failed                           */
+  FRM_ERR_NOT_READY = 5,        /* frm_render before frm_resize / frm_set_parameters  */
+  FRM_ERR_BUFFER_TOO_SMALL = 6, /* destination smaller than the frame or band set      */
+  FRM_ERR_UNSUPPORTED = 7       /* e.g. num_iterations above FRM_MAX_NUM_ITERATIONS    */
+};
+
+/* ---- the reference's uniform, byte for byte -------------------------------
+ * src/parameters.rs:6-15 (#[repr(C)], bytemuck Pod) mirrored in WGSL at
+ * src/fragment.wgsl:108-116. Offsets: camera_matrix 0, aspect_scale 64, time 72,
+ * num_iterations 76, scene_index 80, padding 84; sizeof == 96.
+ * camera_matrix holds the TRANSPOSE of the cgmath camera matrix in column-major
+ * order (parameters.rs:23-25), i.e. camera_matrix[4*j + i] = C[row j][col i]; the
+ * kernel computes C·v exactly like `(v * camera_matrix)` in fragment.wgsl:315-317. */
+typedef struct frm_parameters {
+  float camera_matrix[16];
+  float aspect_scale[2];
+  float time;
+  uint32_t num_iterations;
+  uint32_t scene_index;
+  uint8_t padding[12];
+} frm_parameters;
+
+#ifdef __cplusplus
+static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
+static_assert(offsetof(frm_parameters, aspect_scale) == 64, "aspect_scale @64");
+static_assert(offsetof(frm_parameters, time) == 72, "time @72");
+static_assert(offsetof(frm_parameters, num_iterations) == 76, "num_iterations @76");
+static_assert(offsetof(frm_parameters, scene_index) == 80, "scene_index @80");
+#else
+_Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
+#endif
+
+#define FRM_NUM_SCENES 19u            /* parameters.rs:35 (NUM_SCENES)                 */
+#define FRM_DEFAULT_MAX_STEPS 5000u   /* fragment.wgsl:4 (MAX_ITERATIONS)              */
+#define FRM_MAX_NUM_ITERATIONS 4096u  /* guard: fractal loops are O(num_iterations)    */
+#define FRM_MAX_DIMENSION 32768u      /* width/height limit per frame                  */
+
+/* config flags */
+#define FRM_FLAG_SCENE_SPHERE 0x1u  /* build-only extension scene for BASELINE config C1:
+                                       DE = length(p) - 0.5, colour = colorize(p). Not in
+                                       the reference (its out-of-range scene ids map to 0). */
+#define FRM_FLAG_SIMPLE_KERNEL 0x2u /* use the one-thread-per-pixel kernel instead of the
+                                       persistent ray-regeneration kernel (same bytes). */
+
+typedef struct frm_config {
+  int32_t device;     /* HIP device ordinal (replaces the wgpu adapter request,
+                         persistent_graphics.rs:43-50)                                 */
+  uint32_t max_steps; /* march() step cap; 0 = FRM_DEFAULT_MAX_STEPS. It also feeds the
+                         ambient-occlusion term (fragment.wgsl:289,342)               */
+  uint32_t flags;     /* FRM_FLAG_*                                                    */
+  uint32_t reserved;  /* must be 0                                                     */
+} frm_config;
+
+/* Work counters of one render (exact; equal to the CPU oracle's counts). */
+typedef struct frm_stats {
+  uint64_t pixels;          /* pixels shaded                                           */
+  uint64_t hit_pixels;      /* primary march hits (distance >= 0, fragment.wgsl:334)   */
+  uint64_t primary_steps;   /* scene() evaluations inside the primary march loop       */
+  uint64_t shadow_steps;    /* scene() evaluations inside the shadow march loop        */
+  uint64_t normal_evals;    /* scene() evaluations in calculate_normal (4 per hit)     */
+  uint64_t fractal_bodies;  /* Mandelbulb loop bodies that ran to completion           */
+  uint64_t fractal_bailouts;/* Mandelbulb loop exits by bailout                        */
+  uint64_t march_steps;     /* primary_steps + shadow_steps (the headline unit)        */
+  uint64_t wom_ops;         /* algorithmic VALU lane-ops of the frame */
+  double kernel_ms;         /* device time of the render kernel(s) (HIP events)        */
+} frm_stats;
+
+typedef struct frm_ctx frm_ctx;
+
+/* ---- lifecycle (replaces Graphics::init, graphics.rs:25-37) ------------------ */
+int frm_create(frm_ctx** out_ctx, const frm_config* config);
+int frm_destroy(frm_ctx* ctx);
+const char* frm_last_error(const frm_ctx* ctx);
+uint32_t frm_abi_version(void);
+int frm_device_count(int32_t* out_count);
+
+/* ---- frame size (replaces BlitGraphics::init / update_render_texture_size,
+ *      graphics.rs:54-57, render_texture_config.rs:1-22). Allocates the device
+ *      RGBA8 framebuffer, pitch = 4*width. The caller sets aspect_scale with
+ *      frm_parameters_update_aspect(width, height) semantics (parameters.rs:18-21). */
+int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height);
+
+/* ---- uniform upload (replaces Graphics::update_parameters_buffer,
+ *      graphics.rs:59-61 → queue.write_buffer, persistent_graphics.rs:167-173).
+ *      The struct is copied; it reaches the kernel by value. */
+int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters);
+
+/* ---- draw (replaces Graphics::render, graphics.rs:91-110). One full frame into
+ *      the context framebuffer. stats == NULL: asynchronous. stats != NULL: waits
+ *      for the frame and fills the counters and kernel time. */
+int frm_render(frm_ctx* ctx, frm_stats* stats);
+
+/* ---- readback (replaces the blit pass + present, graphics.rs:101-108). Copies the
+ *      whole RGBA8 sRGB frame (row 0 = top, 4*width*height bytes) to host memory. */
+int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes);
+int frm_synchronize(frm_ctx* ctx);
+
+/* ---- row-tiled rendering for multi-GPU (no reference counterpart: the reference
+ *      is single-device). Band b covers frame rows [b*band_rows, (b+1)*band_rows).
+ *      This call renders bands first_band, first_band+band_stride, ... (below
+ *      num_bands(H)) and stores them back to back, band-major, at dev_dst (device
+ *      memory of this context's GPU), each row 4*width bytes. `stream` is a
+ *      hipStream_t (NULL = context stream). dev_counters, if not NULL, is device
+ *      memory of FRM_NUM_COUNTERS uint64 to which the work counters are ADDED.
+ *      Asynchronous. */
+#define FRM_NUM_COUNTERS 8u
+int frm_band_rows_for(uint32_t height, uint32_t band_rows, uint32_t first_band,
+                      uint32_t band_stride, uint32_t* out_rows);
+int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t band_rows,
+                     uint32_t first_band, uint32_t band_stride, void* stream,
+                     uint64_t* dev_counters);
+/* Reassemble a frame from per-rank band buffers laid out rank-major in dev_src
+ * (rank r's buffer starts at r*rank_stride_bytes, as written by frm_render_bands with
+ * first_band = r, band_stride = ranks) into row-major dev_dst. Asynchronous. */
+int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride_bytes,
+                        uint8_t* dev_dst, size_t dst_bytes, uint32_t band_rows,
+                        uint32_t ranks, void* stream);
+/* Convert FRM_NUM_COUNTERS raw counters (host copy) to frm_stats for the context's
+ * current parameters (fills wom_ops; kernel_ms = 0). */
+int frm_stats_from_counters(const frm_ctx* ctx, const uint64_t* counters, frm_stats* out);
+
+/* ---- diagnostics (parity tooling; synchronous, host pointers) -------------------
+ * frm_eval_scene: evaluates the current scene's distance estimator and object colour
+ * (scene(position), fragment.wgsl:18-78) at n points (xyz interleaved) on the GPU.
+ * frm_eval_math: evaluates one frm builtin on the GPU, element-wise; fn = FRM_MATH_*. */
+enum {
+  FRM_MATH_SIN = 0, FRM_MATH_COS = 1, FRM_MATH_ACOS = 2, FRM_MATH_ATAN2 = 3,
+  FRM_MATH_LOG = 4, FRM_MATH_LOG2 = 5, FRM_MATH_EXP2 = 6, FRM_MATH_POW = 7,
+  FRM_MATH_SQRT = 8, FRM_MATH_DIV = 9
+};
+int frm_eval_scene(frm_ctx* ctx, const float* points, uint32_t n, float* out_distance,
+                   float* out_color);
+int frm_eval_math(frm_ctx* ctx, int32_t fn, const float* a, const float* b, uint32_t n,
+                  float* out);
+
+/* ---- host-side mirrors of the reference's Parameters mutators (src/parameters.rs).
+ *      These let a C/C++/Python host drive the same uniform without Rust. */
+void frm_parameters_default(frm_parameters* p);                               /* #[derive(Default)] */
+void frm_parameters_update_aspect(frm_parameters* p, uint32_t w, uint32_t h); /* parameters.rs:18-21 */
+void frm_parameters_update_time(frm_parameters* p, float delta);             /* parameters.rs:27-29 */
+void frm_parameters_update_num_iterations(frm_parameters* p, int32_t delta); /* parameters.rs:31-33 */
+void frm_parameters_update_scene_index(frm_parameters* p, int32_t delta);    /* parameters.rs:37-40 */
+/* parameters.rs:23-25 with Camera::to_matrix (camera.rs:26-44):
+ * camera_matrix = transpose(T(position) * Ry(yaw) * Rx(pitch)), column-major. */
+void frm_parameters_update_camera(frm_parameters* p, const float position[3], float yaw,
+                                  float pitch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRM_H */
