@@ -75,7 +75,7 @@ def cpu_baseline(params, w, seconds):
         "unit": "Gray-march-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{len(rows)} evenly spaced rows (every {stride}th) of the {w.width}x{w.height} frame, "
+        "sample": f"{len(rows)} evenly spaced rows (one in {stride}) of the {w.width}x{w.height} frame, "
                   f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O2, {threads} threads",
         "frames_per_s_extrapolated": (len(rows) / w.height) / dt,
     }
@@ -116,7 +116,10 @@ def main():
     if world > 1 and rank == 0:
         gathered = [torch.empty(world * nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
         frame = torch.empty(w.height * w.width * 4, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream()
+    # A dedicated stream: its handle is non-null, so libfrm launches on it (a NULL handle
+    # means "the context's own stream") and the HIP events below bracket the kernels.
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
 

@@ -170,34 +170,43 @@ FRM_HD float de_koch(const SceneUniforms& u, v3 p) {
   return tetrahedron(u, q) / u.koch_scale;
 }
 
-// mandelbulb(position, power, bailout), fragment.wgsl:240-271. N+1 bodies; pow(r, y)
-// is exp2(y*log2(r)) (frm semantics), so log2(r) is shared by both pows.
+// One Mandelbulb loop body (fragment.wgsl:251-267) at magnitude r = length(z) <= bailout:
+// updates z and dr in place. pow(r, y) is exp2(y*log2(r)) (frm semantics), so log2(r)
+// is shared by both pows.
+FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+  float theta = acos_(z.z / r);
+  float phi = atan2_(z.y, z.x);
+  float l2 = log2_(r);
+  dr = fma_(exp2_(Pm1 * l2) * P, dr, 1.0f);
+  float er = exp2_(P * l2);
+  float st, ct, sp, cp;
+  sincos_(theta * P, &st, &ct);
+  sincos_(phi * P, &sp, &cp);
+  z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
+}
+// distance = 0.5 * log(magnitude) * magnitude / magnitude_derivative, fragment.wgsl:269
+FRM_HD float mb_distance(float r, float dr) { return ((0.5f * log_(r)) * r) / dr; }
+
+// mandelbulb(position, power, bailout), fragment.wgsl:240-271: N+1 bodies; the distance
+// uses the last magnitude computed at the top of the loop.
 template <bool ITERS>
 FRM_HD float de_mandelbulb(const SceneUniforms& u, v3 p, DeCount& cnt) {
   const uint32_t n = iterations<ITERS>(u.n);
   v3 z = p;
   float dr = 1.0f;
   float r = 0.0f;
-  const float P = u.mb_power, Pm1 = u.mb_power_m1;
   for (uint32_t i = 0;; ++i) {
     r = length(z);
     if (r > u.mb_bailout) {
       cnt.bailouts++;
       break;
     }
-    float theta = acos_(z.z / r);
-    float phi = atan2_(z.y, z.x);
-    float l2 = log2_(r);
-    dr = fma_(exp2_(Pm1 * l2) * P, dr, 1.0f);
-    float er = exp2_(P * l2);
-    float st, ct, sp, cp;
-    sincos_(theta * P, &st, &ct);
-    sincos_(phi * P, &sp, &cp);
-    z = mk(fma_(er, st * cp, p.x), fma_(er, sp * st, p.y), fma_(er, ct, p.z));
+    mb_body(u, p, r, z, dr);
     cnt.bodies++;
     if (i == n) break;
   }
-  return ((0.5f * log_(r)) * r) / dr;
+  return mb_distance(r, dr);
 }
 
 FRM_HD float de_sphere(v3 p) { return length(p) - 0.5f; }
@@ -253,19 +262,21 @@ FRM_HD v3 normal_tap_pos(v3 p, int k) {
   }
 }
 
-// Final colour of a hit pixel given the primary colour, camera direction, normal,
-// primary step count and the shadow march result. fragment.wgsl:337-346.
-FRM_HD v3 shade_hit(const FrameUniforms& f, v3 color, v3 dir, v3 n, uint32_t steps,
-                    float sun_distance, float sun_closeness) {
+// Shading of a hit pixel, fragment.wgsl:337-346, split at the shadow march:
+// shade_hit_pre runs before it (specular term, ambient occlusion), shade_hit_post after.
+FRM_HD v3 shade_hit_pre(const FrameUniforms& f, v3 color, v3 dir, v3 n, uint32_t steps, float* specular) {
   v3 halfway = normalize(-dir + to_sun());
-  float specular = pow_(max_(dot(halfway, n), 0.0f), kSpecularSharpness);
+  *specular = pow_(max_(dot(halfway, n), 0.0f), kSpecularSharpness);
   float ao = pow_(1.0f - (float)steps / f.max_steps_f, kAOSharpness);
-  color = color * mix_(kAOFactor, 1.0f, ao);
+  return color * mix_(kAOFactor, 1.0f, ao);
+}
+FRM_HD v3 shade_hit_post(v3 color, float specular, float sun_distance, float sun_closeness) {
   float shadow = ((sun_distance < 0.0f ? 1.0f : 0.0f) * kShadowSharpness) * sun_closeness;
   color = color * mix_(kShadowFactor, 1.0f, clamp_(shadow, 0.0f, 1.0f));
   float add = ((kSpecularFactor * shadow) * specular) * 1.0f;
   return mk(color.x + add, color.y + add, color.z + add);
 }
+
 // Shadow-ray origin: object_position + object_normal * 2 * MIN_DISTANCE (contracted).
 FRM_HD v3 shadow_origin(v3 pos, v3 n) {
   return mk(fma_(n.x * 2.0f, kMinDistance, pos.x), fma_(n.y * 2.0f, kMinDistance, pos.y),
@@ -332,8 +343,10 @@ FRM_HD v3 shade_pixel(const FrameUniforms& f, const SceneUniforms& su, uint32_t 
     float d3 = scene_de<FAM, ITERS>(su, normal_tap_pos(m.pos, 3), pc.de);
     pc.normal += 4;
     v3 n = normal_from_taps(d0, d1, d2, d3);
+    float spec;
+    color = shade_hit_pre(f, color, dir, n, m.steps, &spec);
     MarchState sun = march<FAM, ITERS, true>(su, f.max_steps, shadow_origin(m.pos, n), to_sun(), pc.de, pc.shadow);
-    color = shade_hit(f, color, dir, n, m.steps, sun.hit ? sun.total : -kInfinity, sun.closeness);
+    color = shade_hit_post(color, spec, sun.hit ? sun.total : -kInfinity, sun.closeness);
   }
   return color;
 }
