@@ -88,6 +88,7 @@ def main():
 
     import frm
     from frm import tiling
+    from frm.distributed import RowTiledFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,64 +108,40 @@ def main():
     r.update_parameters_buffer(params)
 
     band_rows = args.band_rows or (w.height if world == 1 else tiling.choose_band_rows(w.height, world))
-    rows_local = tiling.rank_buffer_rows(w.height, band_rows, world)
-    nbytes = rows_local * w.width * 4
     dev = torch.device("cuda", local)
-    bufs = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2 if world > 1 else 1)]
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
-    frame = gathered = None
-    if world > 1 and rank == 0:
-        gathered = [torch.empty(world * nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-        frame = torch.empty(w.height * w.width * 4, dtype=torch.uint8, device=dev)
     # A dedicated stream: its handle is non-null, so libfrm launches on it (a NULL handle
     # means "the context's own stream") and the HIP events below bracket the kernels.
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    kev = []  # (start, stop) HIP events around every render launch of the timed region
+    timing = {"on": False}
 
-    def render(k, timed):
-        buf = bufs[k % len(bufs)]
-        if timed:
-            kev[k][0].record(stream)
-        r.render_bands(buf.data_ptr(), nbytes, band_rows, rank, world, stream.cuda_stream,
-                       counters.data_ptr())
-        if timed:
-            kev[k][1].record(stream)
-        if world == 1:
-            return None
-        glist = None
-        if rank == 0:
-            g = gathered[k % 2]
-            glist = [g[i * nbytes:(i + 1) * nbytes] for i in range(world)]
-        return dist.gather(buf, gather_list=glist, dst=0, async_op=True)
+    def render_bands(buf, br, first, stride):
+        ev = None
+        if timing["on"]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(stream)
+        r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, stream.cuda_stream, counters.data_ptr())
+        if ev is not None:
+            ev[1].record(stream)
+            kev.append(ev)
 
-    def finish(k, work):
-        if work is None:
-            return
-        work.wait()
-        if rank == 0:
-            r.unshuffle_bands(gathered[k % 2].data_ptr(), nbytes, frame.data_ptr(), frame.numel(),
-                              band_rows, world, stream.cuda_stream)
+    def unshuffle(gathered, frame):
+        r.unshuffle_bands(gathered.data_ptr(), gathered.numel() // world, frame.data_ptr(), frame.numel(),
+                          band_rows, world, stream.cuda_stream)
 
-    def run(n, timed):
-        pending = None
-        for k in range(n):
-            work = render(k, timed)
-            if pending is not None:
-                finish(*pending)
-            pending = (k, work)
-        if pending is not None:
-            finish(*pending)
+    tf = RowTiledFrame(w.width, w.height, rank, world, band_rows, dev, render_bands, unshuffle)
 
-    run(args.warmup, False)
+    tf.run(args.warmup)
     torch.cuda.synchronize()
     counters.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    timing["on"] = True
     t0 = time.perf_counter()
-    run(args.steps, True)
+    tf.run(args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:

@@ -1,0 +1,73 @@
+"""Multi-GPU frame pipeline: one process per GPU; rank r renders the
+interleaved row bands r, r+P, r+2P, ... of every frame into a local buffer, the buffers
+are gathered to rank 0 with torch.distributed (RCCL over xGMI on MI355X, gloo in the CPU
+tests) and rank 0 reassembles the frame. Frame k's gather overlaps frame k+1's render:
+two local buffers and two gather targets alternate, and rank 0 unshuffles frame k only
+after issuing frame k+1's render.
+
+The band renderer and the unshuffle are injected (libfrm on the GPU, the oracle/numpy in
+tests) so the scheduling logic here is exactly what bench.py runs."""
+import torch
+import torch.distributed as dist
+
+from . import tiling
+
+
+class RowTiledFrame:
+    def __init__(self, width, height, rank, world, band_rows, device, render_bands, unshuffle,
+                 group=None):
+        """render_bands(buf, band_rows, first_band, band_stride): enqueue the render of this
+        rank's bands into the uint8 tensor buf (device memory for the GPU path).
+        unshuffle(gathered, frame): rank 0 only; rank-major band buffers -> row-major frame."""
+        self.width, self.height = width, height
+        self.rank, self.world = rank, world
+        self.band_rows = band_rows
+        self.render_bands = render_bands
+        self.unshuffle = unshuffle
+        self.group = group
+        self.rows_local = tiling.rank_buffer_rows(height, band_rows, world)
+        self.nbytes = self.rows_local * width * 4
+        nbuf = 2 if world > 1 else 1
+        self.bufs = [torch.zeros(self.nbytes, dtype=torch.uint8, device=device) for _ in range(nbuf)]
+        self.gathered = self.frame = None
+        if world > 1 and rank == 0:
+            self.gathered = [torch.zeros(world * self.nbytes, dtype=torch.uint8, device=device)
+                             for _ in range(2)]
+            self.frame = torch.zeros(height * width * 4, dtype=torch.uint8, device=device)
+        self.frames_done = 0
+
+    def _issue(self, k):
+        buf = self.bufs[k % len(self.bufs)]
+        self.render_bands(buf, self.band_rows, self.rank, self.world)
+        if self.world == 1:
+            return None
+        glist = None
+        if self.rank == 0:
+            g = self.gathered[k % 2]
+            glist = [g[i * self.nbytes:(i + 1) * self.nbytes] for i in range(self.world)]
+        return dist.gather(buf, gather_list=glist, dst=0, group=self.group, async_op=True)
+
+    def _finish(self, k, work):
+        if work is not None:
+            work.wait()
+            if self.rank == 0:
+                self.unshuffle(self.gathered[k % 2], self.frame)
+        self.frames_done += 1
+
+    def run(self, n):
+        """Render, gather and reassemble n frames (asynchronous on the GPU path: callers
+        synchronize the device to wait for the last one)."""
+        pending = None
+        for k in range(n):
+            work = self._issue(k)
+            if pending is not None:
+                self._finish(*pending)
+            pending = (k, work)
+        if pending is not None:
+            self._finish(*pending)
+
+    def output(self):
+        """Rank 0: the last frame, flat RGBA8 (the band buffer itself when world == 1)."""
+        if self.world == 1:
+            return self.bufs[0]
+        return self.frame

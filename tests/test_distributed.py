@@ -1,0 +1,91 @@
+"""Row-tiled multi-rank pipeline (frm.distributed.RowTiledFrame, the code bench.py runs
+over RCCL) with world_size 2 on gloo, bands rendered by the CPU oracle: the gathered frame
+equals the single-process frame byte for byte (tiling invariance) and the summed work
+counters equal the full frame's."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, W, H, band_rows, q):
+    for p in (ROOT, os.path.join(ROOT, "fractal-ray-marching_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import frm
+    from frm import tiling
+    from frm.distributed import RowTiledFrame
+    from helpers import params_for
+    from oracle import frm_oracle
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    p = params_for(18, 8, frm.POWER8_TIME, W, H)
+    counters = np.zeros(8, np.int64)
+
+    def render_bands(buf, br, first, stride):
+        rows = tiling.global_rows(H, br, first, stride)
+        valid = [y for y in rows if y >= 0]
+        r = frm_oracle.render(p, W, H, 128, rows=valid, threads=2)
+        out = buf.numpy().reshape(-1, W, 4)
+        out[:len(valid)] = r["rgba"]  # padding rows (y < 0) are only at the end
+        counters[:] += r["counters"].astype(np.int64)
+
+    def unshuffle(gathered, frame):
+        g = gathered.numpy().reshape(world, -1, W, 4)
+        frame.numpy()[:] = tiling.unshuffle(g, H, br_used, world).reshape(-1)
+
+    br_used = band_rows
+    tf = RowTiledFrame(W, H, rank, world, band_rows, "cpu", render_bands, unshuffle)
+    tf.run(3)
+    c = torch.from_numpy(counters.copy())
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        q.put((tf.output().numpy().copy(), c.numpy().copy(), tf.frames_done))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,H,band_rows", [(48, 27, 4), (40, 24, 6)])
+def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows):
+    from helpers import params_for
+    import frm
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    frame, counters, frames = q.get(timeout=180)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref = oracle.render(params_for(18, 8, frm.POWER8_TIME, W, H), W, H, 128)
+    assert np.array_equal(frame.reshape(H, W, 4), ref["rgba"])
+    assert frames == 3
+    assert [int(v) for v in counters] == [3 * int(v) for v in ref["counters"]]
+
+
+def test_tiling_geometry_roundtrip():
+    from frm import tiling
+    for H, br, P in [(2160, 15, 8), (27, 4, 2), (7, 3, 4), (4320, 45, 8), (16384, 64, 8)]:
+        seen = []
+        for r in range(P):
+            rows = tiling.global_rows(H, br, r, P)
+            assert len(rows) == tiling.rank_rows(H, br, r, P) <= tiling.rank_buffer_rows(H, br, P)
+            seen += [y for y in rows if y >= 0]
+        assert sorted(seen) == list(range(H))
+    assert tiling.choose_band_rows(2160, 8) == 18 and tiling.choose_band_rows(4320, 8) == 18
+    assert tiling.choose_band_rows(16384, 8) == 16 and tiling.choose_band_rows(1080, 3) == 18

@@ -1,0 +1,59 @@
+"""Summarise rocprofv3 --pmc passes (tools/pmc.sh output) for the render kernel.
+
+Derived values follow MI355X_MICROARCH.md: GRBM_GUI_ACTIVE is summed over the 8 XCDs;
+VALU lane utilisation = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64); VALU busy =
+SQ_ACTIVE_INST_VALU * 2 cycles (wave64 on SIMD32) / (1024 SIMDs * GRBM_GUI_ACTIVE / 8);
+WRITE_SIZE/FETCH_SIZE are in KiB (FETCH_SIZE doubled for gfx950's half-counted reads)."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def load(d, name):
+    files = glob.glob(f"{d}/{name}/**/*counter_collection.csv", recursive=True)
+    if not files:
+        return {}
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(files[0])):
+        if "render" in r["Kernel_Name"]:
+            agg[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    # average over the dispatches of the render kernel
+    out = collections.defaultdict(float)
+    for c in agg.values():
+        for k, v in c.items():
+            out[k] += v / len(agg)
+    return dict(out)
+
+
+def main(d):
+    c = {}
+    for n in ("sq", "sq2", "wr", "rd"):
+        c.update(load(d, n))
+    trace = glob.glob(f"{d}/sq/**/*kernel_trace.csv", recursive=True)
+    dur = []
+    for r in csv.DictReader(open(trace[0])):
+        if "render" in r["Kernel_Name"]:
+            dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    t = sum(dur) / len(dur)
+    grbm_xcd = c["GRBM_GUI_ACTIVE"] / 8
+    s = {
+        "kernel_s_profiled": t,
+        "clock_ghz": grbm_xcd / t / 1e9,
+        "valu_wave_insts": c["SQ_INSTS_VALU"],
+        "valu_lane_utilization": c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64),
+        "valu_busy": c["SQ_ACTIVE_INST_VALU"] * 2 / (1024 * grbm_xcd),
+        "salu_insts": c.get("SQ_INSTS_SALU"),
+        "waves": c["SQ_WAVES"],
+        "wait_inst_any_frac": c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"],
+        "hbm_write_bytes": c.get("WRITE_SIZE", 0) * 1024,
+        "hbm_read_bytes": 2 * c.get("FETCH_SIZE", 0) * 1024,
+        "hbm_write_gbps": c.get("WRITE_SIZE", 0) * 1024 / t / 1e9,
+    }
+    print(json.dumps(s, indent=1))
+    return s
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
