@@ -28,6 +28,8 @@ struct frm_ctx {
   uint8_t* fb = nullptr;
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   unsigned int* queue = nullptr;
+  ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
+  size_t records_cap = 0;
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
@@ -96,10 +98,22 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   return a;
 }
 
-int launch(frm_ctx* ctx, const KernelArgs& a, hipStream_t s) {
+int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
   if (a.g.local_rows == 0) return FRM_OK;
   KernelKind kind = (ctx->flags & FRM_FLAG_SIMPLE_KERNEL) ? kKernelSimple : kKernelPersistent;
-  if (kind == kKernelPersistent) FRM_HIP(ctx, hipMemsetAsync(ctx->queue, 0, sizeof(unsigned int), s));
+  if (kind == kKernelPersistent) {
+    const size_t need = (size_t)a.g.local_rows * a.f.width;
+    if (need > ctx->records_cap) {  // grows outside the steady state (first frame of a size)
+      FRM_HIP(ctx, hipStreamSynchronize(s));
+      if (ctx->records) FRM_HIP(ctx, hipFree(ctx->records));
+      ctx->records = nullptr;
+      ctx->records_cap = 0;
+      FRM_HIP(ctx, hipMalloc(&ctx->records, need * sizeof(ShadeRecord)));
+      ctx->records_cap = need;
+    }
+    a.records = ctx->records;
+    FRM_HIP(ctx, hipMemsetAsync(ctx->queue, 0, sizeof(unsigned int), s));
+  }
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s));
   return FRM_OK;
 }
@@ -168,6 +182,7 @@ int frm_destroy(frm_ctx* ctx) {
   if (ctx->fb) (void)hipFree(ctx->fb);
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->queue) (void)hipFree(ctx->queue);
+  if (ctx->records) (void)hipFree(ctx->records);
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

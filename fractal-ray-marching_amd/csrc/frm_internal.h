@@ -11,6 +11,16 @@ struct BandGeometry {
   uint32_t band_rows, first_band, band_stride, local_rows;
 };
 
+// Per-pixel result of the persistent march kernel, consumed by the shading pass (32 B).
+struct ShadeRecord {
+  float t, nx, ny, nz;      // primary hit distance, surface normal (written at the last tap)
+  float closeness;          // shadow march closeness
+  uint32_t psteps;          // primary march steps (ambient occlusion)
+  uint32_t flags;           // kRecHit | kRecSunMiss; 0 = primary miss
+  uint32_t pad;
+};
+constexpr uint32_t kRecHit = 1u, kRecSunMiss = 2u;
+
 struct KernelArgs {
   FrameUniforms f;
   SceneUniforms s;
@@ -18,6 +28,7 @@ struct KernelArgs {
   uint32_t* out;                  // packed RGBA8 words, local row-major, pitch = width
   unsigned long long* counters;   // FRM_NUM_COUNTERS, accumulated
   unsigned int* queue;            // persistent kernel: work-queue head (zeroed per launch)
+  ShadeRecord* records;           // persistent kernel: local_rows * width records
   uint32_t tiles_x, tiles_total;  // persistent kernel: 8x8 pixel tiles of the launch
 };
 

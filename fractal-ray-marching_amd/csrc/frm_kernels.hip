@@ -56,140 +56,144 @@ __global__ __launch_bounds__(256) void render_simple(KernelArgs a) {
   }
 }
 
-// ---- persistent ray-regeneration kernel -------------------------------------------
-// One lane = one pixel at a time, driven by a per-lane state machine over the phases of
-// fragment_main (primary march -> 4 normal taps -> shadow march -> shade). Every loop
-// iteration advances every live lane by exactly one unit of DE work: one Mandelbulb loop
-// body (the DE is resumable: z, dr, magnitude, body index live in registers), or one
-// whole DE for the fixed-trip-count families. A lane whose pixel is finished takes the
-// next pixel from a wave-local pool, refilled with one atomic per 8x8 tile from a global
-// queue, so lanes never wait for the slowest ray of their wave (SIMD utilisation) and the
-// Mandelbulb bailout no longer serialises the wave on its longest DE. Per-pixel arithmetic
-// is the same sequence of operations as shade_pixel<>, so the bytes are identical.
+// ---- persistent ray-regeneration kernel + deferred shading pass -------------------
+// march_persistent<FAM>: one lane = one pixel at a time, driven by a per-lane state machine
+// over the phases of fragment_main (primary march -> 4 normal taps -> shadow march).
+// Every loop iteration advances every live lane by exactly one unit of DE work: one
+// Mandelbulb loop body (the DE is resumable: z, dr, magnitude and body index live in
+// registers), or one whole DE for the fixed-trip-count families. A lane whose pixel is
+// done takes the next pixel of its wave's current 8x8 tile; a wave fetches tiles from a
+// global queue with one atomic per 64 pixels, and computes the new tile's 64 camera rays
+// in one coherent pass into LDS. Instead of shading at low lane occupancy, a finished
+// pixel stores a 32-byte ShadeRecord; shade_pass then shades and sRGB-packs all pixels
+// coherently. Per-pixel arithmetic is the same operation sequence as shade_pixel<>, so
+// the bytes are identical to render_simple and the oracle.
 constexpr uint32_t kIdle = 0xFFFFFFFFu;
 constexpr uint32_t kTile = 64u;  // pixels per queue entry (one 8x8 tile)
 
 enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(__ballot(c)); }
 
 template <uint32_t FAM, bool ITERS>
-__global__ __launch_bounds__(256) void render_persistent(KernelArgs a) {
-  __shared__ float table[256];
-  table[threadIdx.x] = kSrgbThresholds[threadIdx.x];
-  __syncthreads();
+__global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
+  __shared__ float4 tile_rays[4][kTile];  // per wave: camera ray xyz + local pixel index bits
 
   const FrameUniforms& f = a.f;
   const SceneUniforms& su = a.s;
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t lane_bit = 1ull << lane;
   const uint32_t total = a.tiles_total * kTile;
   const uint32_t n_iter = iterations<ITERS>(su.n);
+  ShadeRecord* __restrict__ rec = a.records;
 
-  // wave-uniform pixel pool [pool_next, pool_end)
-  uint32_t pool_next = 0, pool_end = 0;
+  // wave-uniform state: current tile and how many of its 64 slots were handed out
+  uint32_t slots_used = kTile;
   bool exhausted = false;
+  uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
 
   // per-lane state
-  uint32_t pix = kIdle;        // local pixel index (x + lr * width) being shaded
+  uint32_t pix = kIdle;      // local pixel index (lr * width + x) being marched
   uint32_t phase = kPrimary;
-  bool need_point = false;     // start a DE at the phase's next sample point
-  bool done = false;           // the current DE has its result
-  v3 o = mk(0.f, 0.f, 0.f), d = o, hp = o, color = o, nsum = o, q = o, z = o;
-  float t = 0.f, closeness = 0.f, spec = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
+  bool need_point = false;   // start a DE at the phase's next sample point
+  bool done = false;         // the current DE has its result
+  v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
+  float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
-  uint32_t c_pix = 0, c_hit = 0, c_prim = 0, c_shadow = 0;
-  DeCount cnt = {0u, 0u};
 
   for (;;) {
-    // 1. refill idle lanes from the pool (one global atomic per 8x8 tile)
-    uint64_t want = __ballot(pix == kIdle);
-    if (want == 0 && exhausted) break;  // unreachable: live lanes keep the wave going
+    // 1. refill idle lanes from the wave's current tile; fetch + ray-gen a new tile
+    const uint64_t want = __ballot(pix == kIdle);
     if (want != 0 && !exhausted) {
-      if (pool_next == pool_end) {
+      if (slots_used == kTile) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(a.queue, kTile);
         base = uniform(__shfl(base, 0, 64));
         if (base >= total) {
           exhausted = true;
         } else {
-          pool_next = base;
-          pool_end = base + kTile;
+          const uint32_t tile = base >> 6;
+          const uint32_t x = (tile % a.tiles_x) * 8u + (lane & 7u);
+          const uint32_t lr = (tile / a.tiles_x) * 8u + (lane >> 3);
+          uint32_t y = 0, p = kIdle;
+          if (x < f.width && lr < a.g.local_rows) {
+            y = band_row_to_global(a.g, lr);
+            if (y < f.height) p = lr * f.width + x;
+          }
+          v3 ray = mk(0.f, 0.f, 0.f);
+          if (p != kIdle) ray = camera_ray(f, x, y);
+          n_pix += count(p != kIdle);
+          tile_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
+          __builtin_amdgcn_wave_barrier();
+          slots_used = 0;
         }
       }
-      if (!exhausted || pool_next != pool_end) {
-        const uint32_t avail = pool_end - pool_next;
-        const uint32_t rank = __popcll(want & (lane_bit - 1ull));
-        if ((want & lane_bit) && rank < avail) {
-          // tile-major pixel order: consecutive indices form 8x8 tiles
-          const uint32_t idx = pool_next + rank, tile = idx >> 6, in = idx & 63u;
-          const uint32_t x = (tile % a.tiles_x) * 8u + (in & 7u);
-          const uint32_t lr = (tile / a.tiles_x) * 8u + (in >> 3);
-          if (x < f.width && lr < a.g.local_rows) {
-            const uint32_t y = band_row_to_global(a.g, lr);
-            if (y < f.height) {
-              pix = lr * f.width + x;
-              c_pix++;
-              d = camera_ray(f, x, y);
-              o = f.origin;
-              t = 0.f;
-              it = 0;
-              phase = kPrimary;
-              need_point = true;
-            }
+      if (slots_used < kTile) {
+        const uint32_t slot = slots_used + __popcll(want & (lane_bit - 1ull));
+        if ((want & lane_bit) && slot < kTile) {
+          const float4 r = tile_rays[wave][slot];
+          pix = __float_as_uint(r.w);
+          if (pix != kIdle) {
+            d = mk(r.x, r.y, r.z);
+            o = f.origin;
+            t = 0.f;
+            it = 0;
+            phase = kPrimary;
+            need_point = true;
           }
         }
-        pool_next += min(avail, (uint32_t)__popcll(want));
+        slots_used = min(kTile, slots_used + (uint32_t)__popcll(want));
       }
     }
 
-    // 2. start the next DE of every lane that needs one
+    // 2. start the next DE of every lane that needs one (the hit point of the normal
+    //    taps is recomputed from the unchanged primary ray: ray_at(o, t_hit, d))
+    bool bail = false;
     if (need_point) {
       need_point = false;
-      q = (phase - kTap0 <= kTap3 - kTap0) ? normal_tap_pos(hp, (int)(phase - kTap0)) : ray_at(o, t, d);
+      const v3 r = ray_at(o, t, d);
+      q = (phase - kTap0 <= kTap3 - kTap0) ? normal_tap_pos(r, (int)(phase - kTap0)) : r;
       if constexpr (FAM == kMandelbulb) {
         z = q;
         dr = 1.f;
         body = 0;
         mag = length(q);
         done = mag > su.mb_bailout;
-        if (done) cnt.bailouts++;
+        bail = done;
       } else {
-        de = scene_de<FAM, ITERS>(su, q, cnt);
+        DeCount unused = {0u, 0u};
+        de = scene_de<FAM, ITERS>(su, q, unused);
         done = true;
       }
     }
 
     // 3. one Mandelbulb body for every lane with a DE in flight
+    bool did_body = false;
     if constexpr (FAM == kMandelbulb) {
       if (pix != kIdle && !done) {
+        did_body = true;
         mb_body(su, q, mag, z, dr);
-        cnt.bodies++;
         body++;
         if (body > n_iter) {
           done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
         } else {
           mag = length(z);
-          if (mag > su.mb_bailout) {
-            done = true;
-            cnt.bailouts++;
-          }
+          done = mag > su.mb_bailout;
+          bail = done;
         }
       }
     }
 
-    // 4. consume finished DEs: march / normal / shadow bookkeeping, shading
+    // 4. consume finished DEs: march / normal / shadow bookkeeping
+    bool ev_prim = false, ev_hit = false, ev_shadow = false;
     if (pix != kIdle && done) {
       done = false;
       if constexpr (FAM == kMandelbulb) de = mb_distance(mag, dr);
-      bool finished = false;
-      float sun_distance = 0.f;
       if (phase == kPrimary) {
-        c_prim++;
+        ev_prim = true;
         if (de <= kMinDistance) {  // hit: object_result.distance = t >= 0
-          c_hit++;
-          hp = q;
-          color = scene_color<FAM>(q);
+          ev_hit = true;
           psteps = it;
           phase = kTap0;
           need_point = true;
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(256) void render_persistent(KernelArgs a) {
           if (it < f.max_steps && t < kMaxTotalDistance) {
             need_point = true;
           } else {  // miss: BACKGROUND_COLOR
-            a.out[pix] = 255u << 24;
+            rec[pix].flags = 0u;
             pix = kIdle;
           }
         }
@@ -209,8 +213,9 @@ __global__ __launch_bounds__(256) void render_persistent(KernelArgs a) {
         else if (phase == kTap0 + 2) nsum = mk(nsum.x - de, nsum.y + de, nsum.z - de);
         else nsum = mk(nsum.x + de, nsum.y + de, nsum.z + de);
         if (phase == kTap3) {
-          v3 n = normalize(nsum);
-          color = shade_hit_pre(f, color, d, n, psteps, &spec);
+          const v3 n = normalize(nsum);
+          const v3 hp = ray_at(o, t, d);
+          *reinterpret_cast<float4*>(&rec[pix].t) = make_float4(t, n.x, n.y, n.z);
           o = shadow_origin(hp, n);
           d = to_sun();
           t = 0.f;
@@ -222,36 +227,71 @@ __global__ __launch_bounds__(256) void render_persistent(KernelArgs a) {
         }
         need_point = true;
       } else {  // shadow march toward the sun
-        c_shadow++;
+        ev_shadow = true;
         closeness = min_(closeness, de / t);
+        bool finished = false, sun_miss = false;
         if (de <= kMinDistance) {
           finished = true;
-          sun_distance = t;
         } else {
           t = t + de;
           it++;
-          if (it < f.max_steps && t < kMaxTotalDistance) need_point = true;
-          else {
+          if (it < f.max_steps && t < kMaxTotalDistance) {
+            need_point = true;
+          } else {
             finished = true;
-            sun_distance = -kInfinity;
+            sun_miss = true;
           }
         }
-      }
-      if (finished) {
-        a.out[pix] = pack_rgba(shade_hit_post(color, spec, sun_distance, closeness), table);
-        pix = kIdle;
+        if (finished) {
+          *reinterpret_cast<uint4*>(&rec[pix].closeness) =
+              make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u), 0u);
+          pix = kIdle;
+        }
       }
     }
+    n_body += count(did_body);
+    n_bail += count(bail);
+    n_prim += count(ev_prim);
+    n_hit += count(ev_hit);
+    n_shadow += count(ev_shadow);
 
     if (exhausted && __ballot(pix != kIdle) == 0) break;
   }
 
-  unsigned long long v[7] = {c_pix, c_hit, c_prim, c_shadow, 4ull * c_hit, cnt.bodies, cnt.bailouts};
+  if (lane == 0) {
+    unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    unsigned long long sum = wave_sum(v[k]);
-    if (lane == 0 && sum) atomicAdd(&a.counters[k], sum);
+    for (int k = 0; k < 7; ++k)
+      if (v[k]) atomicAdd(&a.counters[k], v[k]);
   }
+}
+
+// Coherent shading of the records written by march_persistent: fragment.wgsl:333-348
+// (+ the Rgba8UnormSrgb store). One thread per local pixel, row-major.
+template <uint32_t FAM>
+__global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
+  __shared__ float table[256];
+  table[threadIdx.x] = kSrgbThresholds[threadIdx.x];
+  __syncthreads();
+  const uint32_t width = a.f.width;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= a.g.local_rows * width) return;
+  const uint32_t lr = idx / width, x = idx - lr * width;
+  const uint32_t y = band_row_to_global(a.g, lr);
+  if (y >= a.f.height) return;
+  const uint4 r1 = *reinterpret_cast<const uint4*>(&a.records[idx].closeness);
+  uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
+  if (r1.z & kRecHit) {
+    const float4 r0 = *reinterpret_cast<const float4*>(&a.records[idx].t);
+    const v3 dir = camera_ray(a.f, x, y);
+    const v3 hp = ray_at(a.f.origin, r0.x, dir);
+    const v3 n = mk(r0.y, r0.z, r0.w);
+    float spec;
+    v3 color = shade_hit_pre(a.f, scene_color<FAM>(hp), dir, n, r1.y, &spec);
+    color = shade_hit_post(color, spec, (r1.z & kRecSunMiss) ? -kInfinity : 0.0f, __uint_as_float(r1.x));
+    word = pack_rgba(color, table);
+  }
+  a.out[idx] = word;
 }
 
 // dst row y <- band b = y / band_rows, held by rank b % ranks as its (b / ranks)-th band.
@@ -341,7 +381,7 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   static int blocks_per_cu = 0;  // occupancy of this instantiation (per process)
   if (blocks_per_cu == 0) {
     int n = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent<FAM, ITERS>, 256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS>, 256, 0);
     if (e != hipSuccess) return e;
     blocks_per_cu = n > 0 ? n : 1;
   }
@@ -350,7 +390,9 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   const uint32_t max_blocks = (args.tiles_total + 3u) / 4u;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL((render_persistent<FAM, ITERS>), dim3(blocks), dim3(256), 0, stream, args);
+  hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(256), 0, stream, args);
+  const uint32_t pixels = args.g.local_rows * args.f.width;
+  hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u), dim3(256), 0, stream, args);
   return hipGetLastError();
 }
 
