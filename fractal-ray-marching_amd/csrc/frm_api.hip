@@ -7,6 +7,7 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -16,6 +17,10 @@
 #include "frm_internal.h"
 
 using namespace frm;
+
+// Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
+// pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
+static constexpr uint32_t kDefaultServiceMin = 16;  // swept 1..48 on MI355X (round 1)
 
 struct frm_ctx {
   int device = 0;
@@ -30,6 +35,7 @@ struct frm_ctx {
   unsigned int* queue = nullptr;
   ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
   size_t records_cap = 0;
+  uint32_t service_min = kDefaultServiceMin;
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
@@ -95,6 +101,7 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.queue = ctx->queue;
   a.tiles_x = (ctx->width + 7u) / 8u;
   a.tiles_total = a.tiles_x * ((local_rows + 7u) / 8u);
+  a.service_min = ctx->service_min;
   return a;
 }
 
@@ -153,6 +160,10 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   ctx->device = config->device;
   ctx->max_steps = config->max_steps ? config->max_steps : FRM_DEFAULT_MAX_STEPS;
   ctx->flags = config->flags;
+  if (const char* env = getenv("FRM_SERVICE_MIN")) {
+    long v = strtol(env, nullptr, 10);
+    if (v >= 1 && v <= 64) ctx->service_min = (uint32_t)v;
+  }
   int rc = FRM_OK;
   do {
     if ((e = hipSetDevice(ctx->device)) != hipSuccess) { rc = hip_fail(ctx, e, "hipSetDevice"); break; }

@@ -30,6 +30,7 @@ struct KernelArgs {
   unsigned int* queue;            // persistent kernel: work-queue head (zeroed per launch)
   ShadeRecord* records;           // persistent kernel: local_rows * width records
   uint32_t tiles_x, tiles_total;  // persistent kernel: 8x8 pixel tiles of the launch
+  uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
 };
 
 // frm_kernels.hip

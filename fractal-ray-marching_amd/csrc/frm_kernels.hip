@@ -103,90 +103,19 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
   uint32_t it = 0, psteps = 0, body = 0;
 
   for (;;) {
-    // 1. refill idle lanes from the wave's current tile; fetch + ray-gen a new tile
-    const uint64_t want = __ballot(pix == kIdle);
-    if (want != 0 && !exhausted) {
-      if (slots_used == kTile) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.queue, kTile);
-        base = uniform(__shfl(base, 0, 64));
-        if (base >= total) {
-          exhausted = true;
-        } else {
-          const uint32_t tile = base >> 6;
-          const uint32_t x = (tile % a.tiles_x) * 8u + (lane & 7u);
-          const uint32_t lr = (tile / a.tiles_x) * 8u + (lane >> 3);
-          uint32_t y = 0, p = kIdle;
-          if (x < f.width && lr < a.g.local_rows) {
-            y = band_row_to_global(a.g, lr);
-            if (y < f.height) p = lr * f.width + x;
-          }
-          v3 ray = mk(0.f, 0.f, 0.f);
-          if (p != kIdle) ray = camera_ray(f, x, y);
-          n_pix += count(p != kIdle);
-          tile_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
-          __builtin_amdgcn_wave_barrier();
-          slots_used = 0;
-        }
-      }
-      if (slots_used < kTile) {
-        const uint32_t slot = slots_used + __popcll(want & (lane_bit - 1ull));
-        if ((want & lane_bit) && slot < kTile) {
-          const float4 r = tile_rays[wave][slot];
-          pix = __float_as_uint(r.w);
-          if (pix != kIdle) {
-            d = mk(r.x, r.y, r.z);
-            o = f.origin;
-            t = 0.f;
-            it = 0;
-            phase = kPrimary;
-            need_point = true;
-          }
-        }
-        slots_used = min(kTile, slots_used + (uint32_t)__popcll(want));
-      }
-    }
-
-    // 2. start the next DE of every lane that needs one (the hit point of the normal
-    //    taps is recomputed from the unchanged primary ray: ray_at(o, t_hit, d))
-    bool bail = false;
-    if (need_point) {
-      need_point = false;
-      const v3 r = ray_at(o, t, d);
-      q = (phase - kTap0 <= kTap3 - kTap0) ? normal_tap_pos(r, (int)(phase - kTap0)) : r;
-      if constexpr (FAM == kMandelbulb) {
-        z = q;
-        dr = 1.f;
-        body = 0;
-        mag = length(q);
-        done = mag > su.mb_bailout;
-        bail = done;
-      } else {
-        DeCount unused = {0u, 0u};
-        de = scene_de<FAM, ITERS>(su, q, unused);
-        done = true;
-      }
-    }
-
-    // 3. one Mandelbulb body for every lane with a DE in flight
-    bool did_body = false;
+    // Service (refill, start DEs, consume finished DEs) costs the same however many lanes
+    // take part, so for Mandelbulb it runs only once a.service_min lanes are waiting (or
+    // none is still computing); waiting lanes are masked off in the body meanwhile.
+    bool service = true;
     if constexpr (FAM == kMandelbulb) {
-      if (pix != kIdle && !done) {
-        did_body = true;
-        mb_body(su, q, mag, z, dr);
-        body++;
-        if (body > n_iter) {
-          done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
-        } else {
-          mag = length(z);
-          done = mag > su.mb_bailout;
-          bail = done;
-        }
-      }
+      const uint64_t waiting = __ballot((pix == kIdle && !exhausted) || (pix != kIdle && done));
+      const uint64_t busy = __ballot(pix != kIdle && !done);
+      service = busy == 0 || (uint32_t)__popcll(waiting) >= a.service_min;
     }
-
-    // 4. consume finished DEs: march / normal / shadow bookkeeping
+    bool bail = false;
     bool ev_prim = false, ev_hit = false, ev_shadow = false;
+    if (service) {
+    // 1. consume finished DEs: march / normal / shadow bookkeeping
     if (pix != kIdle && done) {
       done = false;
       if constexpr (FAM == kMandelbulb) de = mb_distance(mag, dr);
@@ -249,6 +178,89 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
         }
       }
     }
+    // 2. refill idle lanes from the wave's current tile; fetch + ray-gen a new tile
+    const uint64_t want = __ballot(pix == kIdle);
+    if (want != 0 && !exhausted) {
+      if (slots_used == kTile) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.queue, kTile);
+        base = uniform(__shfl(base, 0, 64));
+        if (base >= total) {
+          exhausted = true;
+        } else {
+          const uint32_t tile = base >> 6;
+          const uint32_t x = (tile % a.tiles_x) * 8u + (lane & 7u);
+          const uint32_t lr = (tile / a.tiles_x) * 8u + (lane >> 3);
+          uint32_t y = 0, p = kIdle;
+          if (x < f.width && lr < a.g.local_rows) {
+            y = band_row_to_global(a.g, lr);
+            if (y < f.height) p = lr * f.width + x;
+          }
+          v3 ray = mk(0.f, 0.f, 0.f);
+          if (p != kIdle) ray = camera_ray(f, x, y);
+          n_pix += count(p != kIdle);
+          tile_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
+          __builtin_amdgcn_wave_barrier();
+          slots_used = 0;
+        }
+      }
+      if (slots_used < kTile) {
+        const uint32_t slot = slots_used + __popcll(want & (lane_bit - 1ull));
+        if ((want & lane_bit) && slot < kTile) {
+          const float4 r = tile_rays[wave][slot];
+          pix = __float_as_uint(r.w);
+          if (pix != kIdle) {
+            d = mk(r.x, r.y, r.z);
+            o = f.origin;
+            t = 0.f;
+            it = 0;
+            phase = kPrimary;
+            need_point = true;
+          }
+        }
+        slots_used = min(kTile, slots_used + (uint32_t)__popcll(want));
+      }
+    }
+
+    // 3. start the next DE of every lane that needs one (the hit point of the normal
+    //    taps is recomputed from the unchanged primary ray: ray_at(o, t_hit, d))
+    if (need_point) {
+      need_point = false;
+      const v3 r = ray_at(o, t, d);
+      q = (phase - kTap0 <= kTap3 - kTap0) ? normal_tap_pos(r, (int)(phase - kTap0)) : r;
+      if constexpr (FAM == kMandelbulb) {
+        z = q;
+        dr = 1.f;
+        body = 0;
+        mag = length(q);
+        done = mag > su.mb_bailout;
+        bail = done;
+      } else {
+        DeCount unused = {0u, 0u};
+        de = scene_de<FAM, ITERS>(su, q, unused);
+        done = true;
+      }
+    }
+
+    }  // service
+
+    // 4. one Mandelbulb body for every lane with a DE in flight
+    bool did_body = false;
+    if constexpr (FAM == kMandelbulb) {
+      if (pix != kIdle && !done) {
+        did_body = true;
+        mb_body(su, q, mag, z, dr);
+        body++;
+        if (body > n_iter) {
+          done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
+        } else {
+          mag = length(z);
+          done = mag > su.mb_bailout;
+          bail = bail || done;
+        }
+      }
+    }
+
     n_body += count(did_body);
     n_bail += count(bail);
     n_prim += count(ev_prim);

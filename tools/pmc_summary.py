@@ -11,13 +11,16 @@ import json
 import sys
 
 
+KERNEL = "render"
+
+
 def load(d, name):
     files = glob.glob(f"{d}/{name}/**/*counter_collection.csv", recursive=True)
     if not files:
         return {}
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(files[0])):
-        if "render" in r["Kernel_Name"]:
+        if KERNEL in r["Kernel_Name"]:
             agg[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     # average over the dispatches of the render kernel
     out = collections.defaultdict(float)
@@ -34,7 +37,7 @@ def main(d):
     trace = glob.glob(f"{d}/sq/**/*kernel_trace.csv", recursive=True)
     dur = []
     for r in csv.DictReader(open(trace[0])):
-        if "render" in r["Kernel_Name"]:
+        if KERNEL in r["Kernel_Name"]:
             dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     t = sum(dur) / len(dur)
     grbm_xcd = c["GRBM_GUI_ACTIVE"] / 8
@@ -56,4 +59,6 @@ def main(d):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2:
+        KERNEL = sys.argv[2]
     main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
