@@ -1,0 +1,104 @@
+// frm_fast.h — device-only fast paths of the frm builtins that are BIT-IDENTICAL to the
+// exact definitions in frm_math.h on restricted operand ranges. The persistent kernel
+// runs mb_body_tame() only when every active lane of the wave has tame operands
+// (mb_tame()); otherwise it runs the exact mb_body(). Results never depend on which
+// path ran (tests/test_gpu_de.py checks the tame path against the oracle).
+//
+// Where the savings come from (hipcc's correctly rounded lowerings, gfx950):
+//  * sqrt: v_sqrt_f32 + a one-ulp correction; the exact lowering also rescales inputs
+//    below 2^-96 (5 instructions) — not needed when x == 0 or x >= 2^-96.
+//  * a / b: the same Newton sequence as the exact lowering, without v_div_scale (returns
+//    its input unchanged when no operand or quotient is near the exponent limits),
+//    v_div_fmas (a plain fma when v_div_scale did not scale) and v_div_fixup (for
+//    finite non-zero operands with a normal quotient it only re-applies the sign).
+//    Zero numerators are handled exactly: 0 / b = +-0 with sign(a) ^ sign(b).
+//  * log2 / exp2: the special-value selects are dead for positive normal finite inputs /
+//    finite exponents, and exp2's clamp cannot change the result for y >= -400 (2^y
+//    then rounds to +0 either way).
+#pragma once
+#include "frm_math.h"
+
+namespace frm {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+
+// Correctly rounded sqrt, exact for x == +-0, x >= 2^-96, +inf, NaN and x < 0 (all x
+// except subnormals and normals below 2^-96). Mirrors LLVM's expansion minus the rescale.
+__device__ __forceinline__ float sqrt_nosmall(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  float s_dn = __uint_as_float(__float_as_uint(s) - 1u);
+  float s_up = __uint_as_float(__float_as_uint(s) + 1u);
+  float r_dn = fmaf(-s_dn, s, x);
+  float r_up = fmaf(-s_up, s, x);
+  s = (r_dn <= 0.0f) ? s_dn : s;
+  s = (r_up > 0.0f) ? s_up : s;
+  return __builtin_amdgcn_class(x, 0x260) ? x : s;  // +-0 and +inf pass through
+}
+
+// Correctly rounded a / b for a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40].
+__device__ __forceinline__ float div_tame(float a, float b) {
+  float r = __builtin_amdgcn_rcpf(b);
+  float e = fmaf(-b, r, 1.0f);
+  r = fmaf(e, r, r);
+  float q = a * r;
+  float rem = fmaf(-b, q, a);
+  q = fmaf(rem, r, q);
+  rem = fmaf(-b, q, a);
+  q = fmaf(rem, r, q);
+  const float zero = __uint_as_float((__float_as_uint(a) ^ __float_as_uint(b)) & 0x80000000u);
+  return (a == 0.0f) ? zero : q;
+}
+
+// acos_ with the exact-for-its-range sqrt (zb is 0 or >= 2^-25 for |t| <= 1; NaN/negative
+// inputs propagate NaN exactly as sqrtf does).
+__device__ __forceinline__ float acos_dev(float t) {
+  float a = fabsf(t);
+  bool big = a > 0.5f;
+  float zb = 0.5f * (1.0f - a);
+  float z = big ? zb : a * a;
+  float w = big ? sqrt_nosmall(zb) : a;
+  float p = fma_(fma_(fma_(fma_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
+                      7.4953002686e-2f), z, 1.6666752422e-1f);
+  float s = fma_(w * z, p, w);
+  float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
+  float rs = kHalfPi - copysignf(s, t);
+  return big ? rb : rs;
+}
+
+// atan2_ for tame x, y (each 0 or with magnitude in [2^-60, 2^40]).
+__device__ __forceinline__ float atan2_tame(float y, float x) {
+  float ax = fabsf(x), ay = fabsf(y);
+  float mx = max_(ax, ay), mn = min_(ax, ay);
+  float a = div_tame(mn, mx);
+  a = (mx == 0.0f) ? 0.0f : a;
+  float s = a * a;
+  float q = fma_(fma_(fma_(fma_(fma_(fma_(fma_(0.002974590389872539f, s, -0.016581183968493302f), s,
+                                      0.04355353931255974f), s, -0.07580578130128461f), s,
+                          0.10678940285181907f), s, -0.14214209135918496f), s,
+                0.1999413720560495f), s, -0.3333316696611865f);
+  float r = fma_(a * s, q, a);
+  r = (ay > ax) ? kHalfPi - r : r;
+  r = (x < 0.0f) ? kPi - r : r;
+  return copysignf(r, y);
+}
+
+// log2_ for positive normal finite x.
+__device__ __forceinline__ float log2_tame(float x) {
+  float f, fe;
+  log_split_(x, &f, &fe);
+  return fma_(log1p_kernel_(f), kLog2e, fe);
+}
+
+// exp2_ for finite y in [-400, 128].
+__device__ __forceinline__ float exp2_tame(float y) {
+  float k = rintf(y);
+  float f = y - k;
+  float p = fma_(fma_(fma_(fma_(fma_(1.535336188319500e-4f, f, 1.339887440266574e-3f), f,
+                               9.618437357674640e-3f), f, 5.550332471162809e-2f), f,
+                     2.402264791363012e-1f), f, 6.931472028550421e-1f);
+  return ldexpf(fma_(f, p, 1.0f), (int)k);
+}
+
+#endif  // __HIP_DEVICE_COMPILE__
+
+}  // namespace frm

@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
         z = q;
         dr = 1.f;
         body = 0;
-        mag = length(q);
+        mag = mb_length(q);
         done = mag > su.mb_bailout;
         bail = done;
       } else {
@@ -249,12 +249,12 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
     if constexpr (FAM == kMandelbulb) {
       if (pix != kIdle && !done) {
         did_body = true;
-        mb_body(su, q, mag, z, dr);
+        mb_step(su, q, mag, z, dr);
         body++;
         if (body > n_iter) {
           done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
         } else {
-          mag = length(z);
+          mag = mb_length(z);
           done = mag > su.mb_bailout;
           bail = bail || done;
         }

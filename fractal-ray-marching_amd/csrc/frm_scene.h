@@ -9,6 +9,7 @@
 // fractal family so the scene switch (fragment.wgsl:19) costs nothing per step.
 #pragma once
 #include "frm_math.h"
+#include "frm_fast.h"
 
 // FRM_ASSUME(c): tell the optimizer c holds (see "ITERS" below).
 #if defined(__clang__)
@@ -188,6 +189,58 @@ FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 // distance = 0.5 * log(magnitude) * magnitude / magnitude_derivative, fragment.wgsl:269
 FRM_HD float mb_distance(float r, float dr) { return ((0.5f * log_(r)) * r) / dr; }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Operands of one Mandelbulb body are tame when r = length(z) is in [2^-40, bailout]
+// and every component of z is 0 or has magnitude >= 2^-60: then z.z / r and
+// min/max(|x|,|y|) are tame divisions, log2(r) has a positive normal argument and both
+// exp2 arguments ((P-1)*log2 r, P*log2 r with P <= 9) lie in [-400, 128].
+__device__ __forceinline__ bool comp_tame(float v) { return v == 0.0f || fabsf(v) >= 0x1p-60f; }
+__device__ __forceinline__ bool mb_tame(v3 z, float r) {
+  return r >= 0x1p-40f && comp_tame(z.x) && comp_tame(z.y) && comp_tame(z.z);
+}
+
+// mb_body (frm_scene.h) with the tame primitives: the same operations in the same order.
+__device__ __forceinline__ void mb_body_tame(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+  float theta = acos_dev(div_tame(z.z, r));
+  float phi = atan2_tame(z.y, z.x);
+  float l2 = log2_tame(r);
+  dr = fma_(exp2_tame(Pm1 * l2) * P, dr, 1.0f);
+  float er = exp2_tame(P * l2);
+  float st, ct, sp, cp;
+  sincos_(theta * P, &st, &ct);
+  sincos_(phi * P, &sp, &cp);
+  z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
+}
+
+// length() with sqrt_nosmall, exact unless 0 < dot(z,z) < 2^-96.
+__device__ __forceinline__ float length_nosmall(v3 a) { return sqrt_nosmall(dot(a, a)); }
+__device__ __forceinline__ bool length_small(v3 a) {
+  float d = dot(a, a);
+  return d > 0.0f && d < 0x1p-96f;
+}
+
+#endif
+
+// One Mandelbulb body; on the GPU the wave takes the tame fast path (frm_fast.h) when all
+// its active lanes have tame operands. Bit-identical to mb_body either way.
+FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (__ballot(!mb_tame(z, r)) == 0) {
+    mb_body_tame(u, c, r, z, dr);
+    return;
+  }
+#endif
+  mb_body(u, c, r, z, dr);
+}
+// length(z) for the Mandelbulb magnitude; fast sqrt unless a lane has 0 < |z|^2 < 2^-96.
+FRM_HD float mb_length(v3 z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (__ballot(length_small(z)) == 0) return length_nosmall(z);
+#endif
+  return length(z);
+}
+
 // mandelbulb(position, power, bailout), fragment.wgsl:240-271: N+1 bodies; the distance
 // uses the last magnitude computed at the top of the loop.
 template <bool ITERS>
@@ -197,12 +250,12 @@ FRM_HD float de_mandelbulb(const SceneUniforms& u, v3 p, DeCount& cnt) {
   float dr = 1.0f;
   float r = 0.0f;
   for (uint32_t i = 0;; ++i) {
-    r = length(z);
+    r = mb_length(z);
     if (r > u.mb_bailout) {
       cnt.bailouts++;
       break;
     }
-    mb_body(u, p, r, z, dr);
+    mb_step(u, p, r, z, dr);
     cnt.bodies++;
     if (i == n) break;
   }

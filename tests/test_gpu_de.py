@@ -69,3 +69,24 @@ def test_scene_de_bit_exact(gpu_renderer_factory, oracle, scene):
         rd, rcol, _ = oracle.scene_de(p, pts, flags=flags)
         assert same_bits(d, rd), f"scene {scene} N={iters}: {np.sum(d.view(np.uint32) != rd.view(np.uint32))} DE mismatches"
         assert same_bits(col, rcol), f"scene {scene} N={iters}: colour mismatch"
+
+
+def test_mandelbulb_tame_and_exact_paths(gpu_renderer_factory, oracle):
+    """Waves whose lanes all have tame operands take the fast body (frm_fast.h); a wave
+    with one non-tame lane (component below 2^-60, |z| below 2^-40, |z|^2 below 2^-96)
+    takes the exact body. Both must equal the oracle."""
+    rng = np.random.default_rng(42)
+    tame = rng.uniform(-1.3, 1.3, size=(64 * 200, 3)).astype(np.float32)
+    odd = tame.copy()
+    odd[::64, 0] = 1e-30          # one tiny component per wave
+    odd[1::64] = [1e-25, 2e-26, -3e-25]  # |z|^2 < 2^-96
+    odd[2::64] = [0.0, 0.0, 1e-13]
+    odd[3::64] = [0.0, 0.0, 0.0]
+    for iters in (3, 12):
+        p = params_for(18, iters, frm.POWER8_TIME, 64, 64)
+        with gpu_renderer_factory() as r:
+            r.update_parameters_buffer(p)
+            for pts in (tame, odd):
+                d, col = r.eval_scene(pts)
+                rd, rcol, _ = oracle.scene_de(p, pts)
+                assert same_bits(d, rd), f"N={iters}: {np.sum(~((d.view(np.uint32) == rd.view(np.uint32)) | (np.isnan(d) & np.isnan(rd))))} mismatches"
