@@ -20,7 +20,7 @@ using namespace frm;
 
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
-static constexpr uint32_t kDefaultServiceMin = 16;  // swept 1..48 on MI355X (round 1)
+static constexpr uint32_t kDefaultServiceMin = 28;  // swept 12..32 on MI355X (round 1)
 
 struct frm_ctx {
   int device = 0;

@@ -77,7 +77,10 @@ __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgc
 __device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(__ballot(c)); }
 
 template <uint32_t FAM, bool ITERS>
-__global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
+#ifndef FRM_MARCH_WAVES_PER_SIMD
+#define FRM_MARCH_WAVES_PER_SIMD 1
+#endif
+__global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
   __shared__ float4 tile_rays[4][kTile];  // per wave: camera ray xyz + local pixel index bits
 
   const FrameUniforms& f = a.f;
@@ -101,24 +104,41 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
   v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
+  uint32_t acc_body = 0, acc_bail = 0;  // per-lane Mandelbulb work counters
 
   for (;;) {
-    // Service (refill, start DEs, consume finished DEs) costs the same however many lanes
-    // take part, so for Mandelbulb it runs only once a.service_min lanes are waiting (or
-    // none is still computing); waiting lanes are masked off in the body meanwhile.
-    bool service = true;
+    // Body phase (Mandelbulb): one loop body per computing lane per iteration, until
+    // a.service_min lanes wait for a service pass (finished DE, or idle with work left)
+    // or no lane computes. The service pass costs the same however many lanes take part.
     if constexpr (FAM == kMandelbulb) {
-      const uint64_t waiting = __ballot((pix == kIdle && !exhausted) || (pix != kIdle && done));
-      const uint64_t busy = __ballot(pix != kIdle && !done);
-      service = busy == 0 || (uint32_t)__popcll(waiting) >= a.service_min;
+      for (;;) {
+        const uint64_t busy = __ballot(pix != kIdle && !done);
+        const uint32_t waiting = exhausted ? (uint32_t)__popcll(__ballot(pix != kIdle && done))
+                                           : 64u - (uint32_t)__popcll(busy);
+        if (busy == 0 || waiting >= a.service_min) break;
+        if (pix != kIdle && !done) {
+          mb_step(su, q, mag, z, dr);
+          body++;
+          if (body > n_iter) {
+            done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
+          } else {
+            mag = mb_length(z);
+            done = mag > su.mb_bailout;
+          }
+        }
+      }
     }
-    bool bail = false;
+
+    // Service pass.
     bool ev_prim = false, ev_hit = false, ev_shadow = false;
-    if (service) {
     // 1. consume finished DEs: march / normal / shadow bookkeeping
     if (pix != kIdle && done) {
       done = false;
-      if constexpr (FAM == kMandelbulb) de = mb_distance(mag, dr);
+      if constexpr (FAM == kMandelbulb) {
+        de = mb_distance(mag, dr);
+        acc_body += body;             // bodies this DE ran (N+1 on a count exit)
+        acc_bail += body <= n_iter;   // exits by bailout (incl. before the first body)
+      }
       if (phase == kPrimary) {
         ev_prim = true;
         if (de <= kMinDistance) {  // hit: object_result.distance = t >= 0
@@ -234,7 +254,6 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
         body = 0;
         mag = mb_length(q);
         done = mag > su.mb_bailout;
-        bail = done;
       } else {
         DeCount unused = {0u, 0u};
         de = scene_de<FAM, ITERS>(su, q, unused);
@@ -242,27 +261,6 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
       }
     }
 
-    }  // service
-
-    // 4. one Mandelbulb body for every lane with a DE in flight
-    bool did_body = false;
-    if constexpr (FAM == kMandelbulb) {
-      if (pix != kIdle && !done) {
-        did_body = true;
-        mb_step(su, q, mag, z, dr);
-        body++;
-        if (body > n_iter) {
-          done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
-        } else {
-          mag = mb_length(z);
-          done = mag > su.mb_bailout;
-          bail = bail || done;
-        }
-      }
-    }
-
-    n_body += count(did_body);
-    n_bail += count(bail);
     n_prim += count(ev_prim);
     n_hit += count(ev_hit);
     n_shadow += count(ev_shadow);
@@ -270,6 +268,10 @@ __global__ __launch_bounds__(256) void march_persistent(KernelArgs a) {
     if (exhausted && __ballot(pix != kIdle) == 0) break;
   }
 
+  if constexpr (FAM == kMandelbulb) {
+    n_body = wave_sum(acc_body);
+    n_bail = wave_sum(acc_bail);
+  }
   if (lane == 0) {
     unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll

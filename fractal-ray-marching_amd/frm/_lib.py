@@ -8,7 +8,8 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfrm.so")
+# FRM_LIB overrides the library path (A/B experiments with alternative builds).
+LIB_PATH = os.environ.get("FRM_LIB") or os.path.join(PKG_ROOT, "lib", "libfrm.so")
 
 FRM_OK = 0
 FRM_ERR_INVALID_ARGUMENT = 1
