@@ -35,6 +35,12 @@ struct frm_ctx {
   unsigned int* queue = nullptr;
   ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
   size_t records_cap = 0;
+  // tile scheduling state (frm_sched.hip): 4 arrays of sched_cap u32 + sort temp space
+  uint32_t* sched = nullptr;
+  void* sched_temp = nullptr;
+  size_t sched_cap = 0, sched_temp_bytes = 0;
+  uint64_t sched_key = 0;  // geometry the recorded tile costs belong to
+  bool sched_history = false;
   uint32_t service_min = kDefaultServiceMin;
   frm_parameters params{};
   bool has_params = false;
@@ -119,7 +125,41 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
       ctx->records_cap = need;
     }
     a.records = ctx->records;
+    // tile scheduling: order this launch's tiles by the cost recorded last time for the
+    // same geometry (most expensive first)
+    const uint32_t tiles = a.tiles_total;
+    if (tiles > ctx->sched_cap) {
+      FRM_HIP(ctx, hipStreamSynchronize(s));
+      if (ctx->sched) FRM_HIP(ctx, hipFree(ctx->sched));
+      if (ctx->sched_temp) FRM_HIP(ctx, hipFree(ctx->sched_temp));
+      ctx->sched = nullptr;
+      ctx->sched_temp = nullptr;
+      ctx->sched_cap = 0;
+      ctx->sched_temp_bytes = schedule_temp_bytes(tiles);
+      FRM_HIP(ctx, hipMalloc(&ctx->sched, (size_t)tiles * 4 * sizeof(uint32_t)));
+      FRM_HIP(ctx, hipMalloc(&ctx->sched_temp, ctx->sched_temp_bytes ? ctx->sched_temp_bytes : 16));
+      ctx->sched_cap = tiles;
+      ctx->sched_history = false;
+    }
+    const uint64_t key = ((uint64_t)a.f.width << 40) ^ ((uint64_t)a.g.local_rows << 20) ^
+                         ((uint64_t)a.g.band_rows << 8) ^ ((uint64_t)a.g.first_band << 4) ^ a.g.band_stride ^
+                         ((uint64_t)a.f.height << 52);
+    const bool history = ctx->sched_history && key == ctx->sched_key;
+    uint32_t* cost = ctx->sched;
+    uint32_t* order = ctx->sched + ctx->sched_cap;
+    FRM_HIP(ctx, schedule_tiles(tiles, history, cost, ctx->sched + 2 * ctx->sched_cap, order,
+                                ctx->sched + 3 * ctx->sched_cap, ctx->sched_temp, ctx->sched_temp_bytes, s));
+    a.tile_order = order;
+    a.tile_cost = cost;
+    ctx->sched_key = key;
+    ctx->sched_history = true;
+    a.debug = (unsigned long long*)(ctx->queue + 8);  // bytes 32..71 of the queue block
     FRM_HIP(ctx, hipMemsetAsync(ctx->queue, 0, sizeof(unsigned int), s));
+#ifdef FRM_STAMPS
+    FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 8, 0, 16, s));
+    FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 12, 0xff, 16, s));  // atomicMin slots
+    FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 16, 0, 8, s));
+#endif
   }
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s));
   return FRM_OK;
@@ -174,7 +214,7 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
     if ((e = hipEventCreate(&ctx->ev_start)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
     if ((e = hipEventCreate(&ctx->ev_stop)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
     if ((e = hipMalloc(&ctx->counters, FRM_NUM_COUNTERS * sizeof(unsigned long long))) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(counters)"); break; }
-    if ((e = hipMalloc(&ctx->queue, 64)) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(queue)"); break; }
+    if ((e = hipMalloc(&ctx->queue, 128)) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(queue)"); break; }
   } while (0);
   if (rc != FRM_OK) {
     g_error = ctx->error;
@@ -194,6 +234,8 @@ int frm_destroy(frm_ctx* ctx) {
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->queue) (void)hipFree(ctx->queue);
   if (ctx->records) (void)hipFree(ctx->records);
+  if (ctx->sched) (void)hipFree(ctx->sched);
+  if (ctx->sched_temp) (void)hipFree(ctx->sched_temp);
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -319,6 +361,12 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
                                 ranks, s));
   return FRM_OK;
 }
+
+#ifdef FRM_STAMPS
+extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
+  return hipMemcpy(out5, ctx->queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int frm_stats_from_counters(const frm_ctx* ctx, const uint64_t* c, frm_stats* out) {
   if (!ctx || !c || !out) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "NULL argument");

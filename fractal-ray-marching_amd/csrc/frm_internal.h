@@ -31,6 +31,9 @@ struct KernelArgs {
   ShadeRecord* records;           // persistent kernel: local_rows * width records
   uint32_t tiles_x, tiles_total;  // persistent kernel: 8x8 pixel tiles of the launch
   uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
+  unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
+  const uint32_t* tile_order;     // persistent kernel: fetch order of the tiles_total tiles
+  uint32_t* tile_cost;            // persistent kernel: max bodies of a pixel, per tile (out)
 };
 
 // frm_kernels.hip
@@ -39,6 +42,11 @@ hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, 
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,
                             uint32_t height, uint32_t band_rows, uint32_t ranks,
                             hipStream_t stream);
+// Tile scheduling (frm_sched.hip): order = tiles by descending cost (previous frame), or
+// the identity when has_history is false. Resets cost to 0 for the next frame.
+hipError_t schedule_tiles(uint32_t tiles, bool has_history, uint32_t* cost, uint32_t* cost_sorted,
+                          uint32_t* order, uint32_t* iota, void* temp, size_t temp_bytes, hipStream_t stream);
+size_t schedule_temp_bytes(uint32_t tiles);
 hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
                              hipStream_t stream);
 hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, float* out, hipStream_t stream);

@@ -105,6 +105,13 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
   uint32_t acc_body = 0, acc_bail = 0;  // per-lane Mandelbulb work counters
+  uint32_t cur_tile = 0;                 // wave-uniform: tile being handed out
+  uint32_t pix_tile = 0, pix_body0 = 0;  // per lane: tile of the pixel, bodies at its start
+#ifdef FRM_STAMPS
+  uint64_t stamp_service = 0, n_service = 0;
+  const uint64_t stamp_begin = __builtin_amdgcn_s_memtime();
+  const uint64_t stamp_real0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   for (;;) {
     // Body phase (Mandelbulb): one loop body per computing lane per iteration, until
@@ -130,6 +137,9 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     }
 
     // Service pass.
+#ifdef FRM_STAMPS  // diagnostic build: wave cycles spent in service passes -> counters[7]
+    const uint64_t stamp0 = __builtin_amdgcn_s_memtime();
+#endif
     bool ev_prim = false, ev_hit = false, ev_shadow = false;
     // 1. consume finished DEs: march / normal / shadow bookkeeping
     if (pix != kIdle && done) {
@@ -153,6 +163,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
             need_point = true;
           } else {  // miss: BACKGROUND_COLOR
             rec[pix].flags = 0u;
+            atomicMax(&a.tile_cost[pix_tile], acc_body - pix_body0 + 1u);
             pix = kIdle;
           }
         }
@@ -194,6 +205,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         if (finished) {
           *reinterpret_cast<uint4*>(&rec[pix].closeness) =
               make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u), 0u);
+          atomicMax(&a.tile_cost[pix_tile], acc_body - pix_body0 + 1u);
           pix = kIdle;
         }
       }
@@ -207,8 +219,13 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         base = uniform(__shfl(base, 0, 64));
         if (base >= total) {
           exhausted = true;
+#ifdef FRM_STAMPS
+          if (lane == 0) atomicMin(a.debug + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
         } else {
-          const uint32_t tile = base >> 6;
+          // the q-th tile fetched is tile_order[q] (most expensive first, from the
+          // previous frame's per-tile cost; identity without history)
+          const uint32_t tile = uniform(a.tile_order[base >> 6]);
           const uint32_t x = (tile % a.tiles_x) * 8u + (lane & 7u);
           const uint32_t lr = (tile / a.tiles_x) * 8u + (lane >> 3);
           uint32_t y = 0, p = kIdle;
@@ -222,6 +239,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           tile_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
           __builtin_amdgcn_wave_barrier();
           slots_used = 0;
+          cur_tile = tile;
         }
       }
       if (slots_used < kTile) {
@@ -230,6 +248,8 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           const float4 r = tile_rays[wave][slot];
           pix = __float_as_uint(r.w);
           if (pix != kIdle) {
+            pix_tile = cur_tile;
+            pix_body0 = acc_body;
             d = mk(r.x, r.y, r.z);
             o = f.origin;
             t = 0.f;
@@ -264,6 +284,10 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     n_prim += count(ev_prim);
     n_hit += count(ev_hit);
     n_shadow += count(ev_shadow);
+#ifdef FRM_STAMPS
+    stamp_service += __builtin_amdgcn_s_memtime() - stamp0;
+    n_service++;
+#endif
 
     if (exhausted && __ballot(pix != kIdle) == 0) break;
   }
@@ -272,6 +296,15 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     n_body = wave_sum(acc_body);
     n_bail = wave_sum(acc_bail);
   }
+#ifdef FRM_STAMPS
+  if (lane == 0) {
+    atomicAdd(&a.counters[7], (unsigned long long)stamp_service);
+    atomicAdd(a.debug, (unsigned long long)(__builtin_amdgcn_s_memtime() - stamp_begin));
+    atomicAdd(a.debug + 1, (unsigned long long)n_service);
+    atomicMin(a.debug + 3, (unsigned long long)stamp_real0);  // first wave start (100 MHz)
+    atomicMax(a.debug + 4, (unsigned long long)__builtin_amdgcn_s_memrealtime());  // last wave end
+  }
+#endif
   if (lane == 0) {
     unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll

@@ -80,3 +80,19 @@ def test_camera_inside_geometry(gpu_renderer_factory, oracle):
         img, _ = gpu_render(gpu_renderer_factory, q, 64, 36, 64)
         ref = oracle.render(q, 64, 36, 64)
         assert np.array_equal(img, ref["rgba"])
+
+
+def test_scheduling_history_does_not_change_bytes(gpu_renderer_factory, oracle):
+    """Frames after the first fetch tiles most-expensive-first (previous frame's costs);
+    the bytes and counters must not change, also after a parameter change (stale order)."""
+    p = params_for(18, 12, frm.POWER8_TIME, 200, 120)
+    q = params_for(18, 8, 1.0, 200, 120, pose="P2")
+    ref_p = oracle.render(p, 200, 120, 256)
+    ref_q = oracle.render(q, 200, 120, 256)
+    with gpu_renderer_factory(max_steps=256) as r:
+        r.resize(200, 120)
+        for params, ref in ((p, ref_p), (p, ref_p), (q, ref_q), (q, ref_q), (p, ref_p)):
+            r.update_parameters_buffer(params)
+            st = r.render()
+            assert np.array_equal(r.read_frame(), ref["rgba"])
+            assert counters_of(st) == [int(c) for c in ref["counters"]]
