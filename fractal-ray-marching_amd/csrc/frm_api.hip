@@ -366,6 +366,12 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
 extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
   return hipMemcpy(out5, ctx->queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
+// per-tile critical-path costs recorded by the last persistent launch (before the next
+// launch resets them)
+extern "C" int frm_debug_tile_costs(frm_ctx* ctx, uint32_t* out, size_t n) {
+  if (n > ctx->sched_cap) n = ctx->sched_cap;
+  return hipMemcpy(out, ctx->sched, n * 4, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
 #endif
 
 int frm_stats_from_counters(const frm_ctx* ctx, const uint64_t* c, frm_stats* out) {

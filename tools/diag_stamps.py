@@ -28,3 +28,13 @@ try:
     print(f"waves {int(out[1])} services; realtime: queue exhausted at {(exhaust-start)/100:.0f} us, last wave ends at {(end-start)/100:.0f} us")
 except AttributeError:
     pass
+try:
+    tiles = ((w.width + 7) // 8) * ((w.height + 7) // 8)
+    costs = np.zeros(tiles, np.uint32)
+    lib.frm_debug_tile_costs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    n = lib.frm_debug_tile_costs(r.ctx, costs.ctypes.data, tiles)
+    c = np.sort(costs[:n])[::-1]
+    print("per-tile max bodies/pixel: max", c[0], "p99.9", c[int(n*0.001)], "p99", c[int(n*0.01)], "p90", c[int(n*0.1)], "median", c[n//2])
+    print("tiles with cost >= half max:", int((c >= c[0] / 2).sum()), "of", n)
+except AttributeError:
+    pass
