@@ -35,11 +35,15 @@ struct frm_ctx {
   unsigned int* queue = nullptr;
   ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
   size_t records_cap = 0;
-  // tile scheduling state (frm_sched.hip): 4 arrays of sched_cap u32 + sort temp space
-  uint32_t* sched = nullptr;
+  // pixel scheduling state (frm_sched.hip), sched_cap entries each: two fetch orders
+  // (the last launch's and the next), the cost keys the last launch recorded per fetch
+  // position, the sort's key output; plus the sort's temp space
+  uint32_t* sched_order[2] = {nullptr, nullptr};
+  uint8_t* sched_keys = nullptr;  // 2 x sched_cap: keys, sorted keys
   void* sched_temp = nullptr;
   size_t sched_cap = 0, sched_temp_bytes = 0;
-  uint64_t sched_key = 0;  // geometry the recorded tile costs belong to
+  int sched_cur = 0;       // sched_order[sched_cur] is the last launch's order
+  uint64_t sched_key = 0;  // geometry the recorded keys belong to
   bool sched_history = false;
   uint32_t service_min = kDefaultServiceMin;
   frm_parameters params{};
@@ -85,6 +89,15 @@ uint32_t band_local_rows(uint32_t height, uint32_t band_rows, uint32_t first, ui
   return count * band_rows;
 }
 
+// Local rows that hold frame rows: all but the missing rows of a short last band, which
+// can only be this launch's last band (its local rows are then a prefix).
+uint32_t band_valid_rows(uint32_t height, const BandGeometry& g) {
+  if (g.local_rows == 0) return 0;
+  const uint32_t last = g.first_band + (g.local_rows / g.band_rows - 1u) * g.band_stride;
+  const uint32_t end = (last + 1u) * g.band_rows;  // one past its last global row
+  return end > height ? g.local_rows - (end - height) : g.local_rows;
+}
+
 int ensure_ready(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
   if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
@@ -105,8 +118,7 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.out = (uint32_t*)dst;
   a.counters = counters;
   a.queue = ctx->queue;
-  a.tiles_x = (ctx->width + 7u) / 8u;
-  a.tiles_total = a.tiles_x * ((local_rows + 7u) / 8u);
+  a.npix = band_valid_rows(ctx->height, a.g) * ctx->width;
   a.service_min = ctx->service_min;
   return a;
 }
@@ -125,32 +137,38 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
       ctx->records_cap = need;
     }
     a.records = ctx->records;
-    // tile scheduling: order this launch's tiles by the cost recorded last time for the
+    // pixel scheduling: fetch this launch's pixels by the cost recorded last time for the
     // same geometry (most expensive first)
-    const uint32_t tiles = a.tiles_total;
-    if (tiles > ctx->sched_cap) {
+    const uint32_t npix = a.npix;
+    if (npix > ctx->sched_cap) {
       FRM_HIP(ctx, hipStreamSynchronize(s));
-      if (ctx->sched) FRM_HIP(ctx, hipFree(ctx->sched));
+      for (auto*& o : ctx->sched_order) {
+        if (o) FRM_HIP(ctx, hipFree(o));
+        o = nullptr;
+      }
+      if (ctx->sched_keys) FRM_HIP(ctx, hipFree(ctx->sched_keys));
       if (ctx->sched_temp) FRM_HIP(ctx, hipFree(ctx->sched_temp));
-      ctx->sched = nullptr;
+      ctx->sched_keys = nullptr;
       ctx->sched_temp = nullptr;
       ctx->sched_cap = 0;
-      ctx->sched_temp_bytes = schedule_temp_bytes(tiles);
-      FRM_HIP(ctx, hipMalloc(&ctx->sched, (size_t)tiles * 4 * sizeof(uint32_t)));
+      ctx->sched_temp_bytes = schedule_temp_bytes(npix);
+      for (auto*& o : ctx->sched_order) FRM_HIP(ctx, hipMalloc(&o, (size_t)npix * sizeof(uint32_t)));
+      FRM_HIP(ctx, hipMalloc(&ctx->sched_keys, (size_t)npix * 2));
       FRM_HIP(ctx, hipMalloc(&ctx->sched_temp, ctx->sched_temp_bytes ? ctx->sched_temp_bytes : 16));
-      ctx->sched_cap = tiles;
+      ctx->sched_cap = npix;
       ctx->sched_history = false;
     }
     const uint64_t key = ((uint64_t)a.f.width << 40) ^ ((uint64_t)a.g.local_rows << 20) ^
                          ((uint64_t)a.g.band_rows << 8) ^ ((uint64_t)a.g.first_band << 4) ^ a.g.band_stride ^
                          ((uint64_t)a.f.height << 52);
     const bool history = ctx->sched_history && key == ctx->sched_key;
-    uint32_t* cost = ctx->sched;
-    uint32_t* order = ctx->sched + ctx->sched_cap;
-    FRM_HIP(ctx, schedule_tiles(tiles, history, cost, ctx->sched + 2 * ctx->sched_cap, order,
-                                ctx->sched + 3 * ctx->sched_cap, ctx->sched_temp, ctx->sched_temp_bytes, s));
-    a.tile_order = order;
-    a.tile_cost = cost;
+    const uint32_t* prev = ctx->sched_order[ctx->sched_cur];
+    uint32_t* next = ctx->sched_order[ctx->sched_cur ^ 1];
+    FRM_HIP(ctx, schedule_pixels(npix, history, ctx->sched_keys, ctx->sched_keys + ctx->sched_cap, prev, next,
+                                 ctx->sched_temp, ctx->sched_temp_bytes, s));
+    ctx->sched_cur ^= 1;
+    a.pixel_order = next;
+    a.pixel_key = ctx->sched_keys;
     ctx->sched_key = key;
     ctx->sched_history = true;
     a.debug = (unsigned long long*)(ctx->queue + 8);  // bytes 32..71 of the queue block
@@ -234,7 +252,9 @@ int frm_destroy(frm_ctx* ctx) {
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->queue) (void)hipFree(ctx->queue);
   if (ctx->records) (void)hipFree(ctx->records);
-  if (ctx->sched) (void)hipFree(ctx->sched);
+  for (uint32_t* o : ctx->sched_order)
+    if (o) (void)hipFree(o);
+  if (ctx->sched_keys) (void)hipFree(ctx->sched_keys);
   if (ctx->sched_temp) (void)hipFree(ctx->sched_temp);
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
@@ -366,11 +386,11 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
 extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
   return hipMemcpy(out5, ctx->queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
-// per-tile critical-path costs recorded by the last persistent launch (before the next
-// launch resets them)
-extern "C" int frm_debug_tile_costs(frm_ctx* ctx, uint32_t* out, size_t n) {
+// per-pixel cost keys recorded by the last persistent launch, by fetch position (before
+// the next launch overwrites them)
+extern "C" int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
   if (n > ctx->sched_cap) n = ctx->sched_cap;
-  return hipMemcpy(out, ctx->sched, n * 4, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+  return hipMemcpy(out, ctx->sched_keys, n, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 #endif
 

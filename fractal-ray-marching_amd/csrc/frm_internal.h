@@ -29,11 +29,11 @@ struct KernelArgs {
   unsigned long long* counters;   // FRM_NUM_COUNTERS, accumulated
   unsigned int* queue;            // persistent kernel: work-queue head (zeroed per launch)
   ShadeRecord* records;           // persistent kernel: local_rows * width records
-  uint32_t tiles_x, tiles_total;  // persistent kernel: 8x8 pixel tiles of the launch
+  uint32_t npix;                  // persistent kernel: pixels of the launch (= fetch positions)
   uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
   unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
-  const uint32_t* tile_order;     // persistent kernel: fetch order of the tiles_total tiles
-  uint32_t* tile_cost;            // persistent kernel: max bodies of a pixel, per tile (out)
+  const uint32_t* pixel_order;    // persistent kernel: local pixel index at each fetch position
+  uint8_t* pixel_key;             // persistent kernel: cost key per fetch position (out)
 };
 
 // frm_kernels.hip
@@ -42,11 +42,13 @@ hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, 
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,
                             uint32_t height, uint32_t band_rows, uint32_t ranks,
                             hipStream_t stream);
-// Tile scheduling (frm_sched.hip): order = tiles by descending cost (previous frame), or
-// the identity when has_history is false. Resets cost to 0 for the next frame.
-hipError_t schedule_tiles(uint32_t tiles, bool has_history, uint32_t* cost, uint32_t* cost_sorted,
-                          uint32_t* order, uint32_t* iota, void* temp, size_t temp_bytes, hipStream_t stream);
-size_t schedule_temp_bytes(uint32_t tiles);
+// Pixel scheduling (frm_sched.hip). With history, next = prev reordered by descending
+// key[i] (the cost key the last launch recorded for the pixel it fetched at position i;
+// stable, one 8-bit radix pass); without, next = 0, 1, ..., npix - 1 (row-major).
+hipError_t schedule_pixels(uint32_t npix, bool has_history, const uint8_t* key, uint8_t* key_sorted,
+                           const uint32_t* prev, uint32_t* next, void* temp, size_t temp_bytes,
+                           hipStream_t stream);
+size_t schedule_temp_bytes(uint32_t npix);
 hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
                              hipStream_t stream);
 hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, float* out, hipStream_t stream);

@@ -62,37 +62,50 @@ __global__ __launch_bounds__(256) void render_simple(KernelArgs a) {
 // Every loop iteration advances every live lane by exactly one unit of DE work: one
 // Mandelbulb loop body (the DE is resumable: z, dr, magnitude and body index live in
 // registers), or one whole DE for the fixed-trip-count families. A lane whose pixel is
-// done takes the next pixel of its wave's current 8x8 tile; a wave fetches tiles from a
-// global queue with one atomic per 64 pixels, and computes the new tile's 64 camera rays
-// in one coherent pass into LDS. Instead of shading at low lane occupancy, a finished
+// done takes the next pixel of its wave's current chunk; a wave fetches chunks of 64
+// pixels from a global queue (one atomic per chunk) in the order frm_sched.hip chose
+// (most expensive pixels first), and computes the chunk's 64 camera rays in one coherent
+// pass into LDS. Instead of shading at low lane occupancy, a finished
 // pixel stores a 32-byte ShadeRecord; shade_pass then shades and sRGB-packs all pixels
 // coherently. Per-pixel arithmetic is the same operation sequence as shade_pixel<>, so
 // the bytes are identical to render_simple and the oracle.
 constexpr uint32_t kIdle = 0xFFFFFFFFu;
-constexpr uint32_t kTile = 64u;  // pixels per queue entry (one 8x8 tile)
+constexpr uint32_t kChunk = 64u;  // pixels per queue fetch (one per lane of the fetching wave)
 
 enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(__ballot(c)); }
 
+// Scheduling key of a finished pixel: 16 x log2(Mandelbulb bodies + 1), 0..255 (~4.4 %
+// steps). Only orders the next frame's fetches; never touches a pixel's bytes.
+__device__ __forceinline__ uint8_t cost_key(uint32_t bodies) {
+  return (uint8_t)min(255.0f, 16.0f * __log2f((float)bodies + 1.0f));
+}
+
+#ifdef FRM_STAMPS
+// diagnostic build: one 8 x u64 record per wave of the last persistent launch
+constexpr uint32_t kWaveDebugSlots = 16384u;
+__device__ unsigned long long g_wave_debug[8u * kWaveDebugSlots];
+#endif
+
 template <uint32_t FAM, bool ITERS>
 #ifndef FRM_MARCH_WAVES_PER_SIMD
 #define FRM_MARCH_WAVES_PER_SIMD 1
 #endif
 __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
-  __shared__ float4 tile_rays[4][kTile];  // per wave: camera ray xyz + local pixel index bits
+  __shared__ float4 chunk_rays[4][kChunk];  // per wave: camera ray xyz + local pixel index bits
 
   const FrameUniforms& f = a.f;
   const SceneUniforms& su = a.s;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t lane_bit = 1ull << lane;
-  const uint32_t total = a.tiles_total * kTile;
+  const uint32_t total = a.npix;
   const uint32_t n_iter = iterations<ITERS>(su.n);
   ShadeRecord* __restrict__ rec = a.records;
 
-  // wave-uniform state: current tile and how many of its 64 slots were handed out
-  uint32_t slots_used = kTile;
+  // wave-uniform state: current chunk of 64 fetched pixels, how many were handed out
+  uint32_t slots_used = kChunk;
   bool exhausted = false;
   uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
 
@@ -105,10 +118,10 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
   uint32_t acc_body = 0, acc_bail = 0;  // per-lane Mandelbulb work counters
-  uint32_t cur_tile = 0;                 // wave-uniform: tile being handed out
-  uint32_t pix_tile = 0, pix_body0 = 0;  // per lane: tile of the pixel, bodies at its start
+  uint32_t cur_base = 0;                 // wave-uniform: fetch position of the chunk's slot 0
+  uint32_t pix_pos = 0, pix_body0 = 0;   // per lane: fetch position of the pixel, bodies at its start
 #ifdef FRM_STAMPS
-  uint64_t stamp_service = 0, n_service = 0;
+  uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
   const uint64_t stamp_begin = __builtin_amdgcn_s_memtime();
   const uint64_t stamp_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -123,6 +136,9 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         const uint32_t waiting = exhausted ? (uint32_t)__popcll(__ballot(pix != kIdle && done))
                                            : 64u - (uint32_t)__popcll(busy);
         if (busy == 0 || waiting >= a.service_min) break;
+#ifdef FRM_STAMPS
+        n_loop++;
+#endif
         if (pix != kIdle && !done) {
           mb_step(su, q, mag, z, dr);
           body++;
@@ -163,7 +179,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
             need_point = true;
           } else {  // miss: BACKGROUND_COLOR
             rec[pix].flags = 0u;
-            atomicMax(&a.tile_cost[pix_tile], acc_body - pix_body0 + 1u);
+            a.pixel_key[pix_pos] = cost_key(acc_body - pix_body0);
             pix = kIdle;
           }
         }
@@ -205,50 +221,48 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         if (finished) {
           *reinterpret_cast<uint4*>(&rec[pix].closeness) =
               make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u), 0u);
-          atomicMax(&a.tile_cost[pix_tile], acc_body - pix_body0 + 1u);
+          a.pixel_key[pix_pos] = cost_key(acc_body - pix_body0);
           pix = kIdle;
         }
       }
     }
-    // 2. refill idle lanes from the wave's current tile; fetch + ray-gen a new tile
+    // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
     const uint64_t want = __ballot(pix == kIdle);
     if (want != 0 && !exhausted) {
-      if (slots_used == kTile) {
+      if (slots_used == kChunk) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.queue, kTile);
+        if (lane == 0) base = atomicAdd(a.queue, kChunk);
         base = uniform(__shfl(base, 0, 64));
         if (base >= total) {
           exhausted = true;
 #ifdef FRM_STAMPS
-          if (lane == 0) atomicMin(a.debug + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+          real_exhaust = __builtin_amdgcn_s_memrealtime();
+          if (lane == 0) atomicMin(a.debug + 2, (unsigned long long)real_exhaust);
 #endif
         } else {
-          // the q-th tile fetched is tile_order[q] (most expensive first, from the
-          // previous frame's per-tile cost; identity without history)
-          const uint32_t tile = uniform(a.tile_order[base >> 6]);
-          const uint32_t x = (tile % a.tiles_x) * 8u + (lane & 7u);
-          const uint32_t lr = (tile / a.tiles_x) * 8u + (lane >> 3);
-          uint32_t y = 0, p = kIdle;
-          if (x < f.width && lr < a.g.local_rows) {
-            y = band_row_to_global(a.g, lr);
-            if (y < f.height) p = lr * f.width + x;
-          }
+          // the i-th pixel fetched is pixel_order[i]: most expensive first (the previous
+          // frame's cost keys, frm_sched.hip), row-major without history
+          uint32_t p = kIdle;
           v3 ray = mk(0.f, 0.f, 0.f);
-          if (p != kIdle) ray = camera_ray(f, x, y);
+          if (base + lane < total) {
+            p = a.pixel_order[base + lane];
+            const uint32_t lr = p / f.width, x = p - lr * f.width;
+            ray = camera_ray(f, x, band_row_to_global(a.g, lr));
+          }
           n_pix += count(p != kIdle);
-          tile_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
+          chunk_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
           __builtin_amdgcn_wave_barrier();
           slots_used = 0;
-          cur_tile = tile;
+          cur_base = base;
         }
       }
-      if (slots_used < kTile) {
+      if (slots_used < kChunk) {
         const uint32_t slot = slots_used + __popcll(want & (lane_bit - 1ull));
-        if ((want & lane_bit) && slot < kTile) {
-          const float4 r = tile_rays[wave][slot];
+        if ((want & lane_bit) && slot < kChunk) {
+          const float4 r = chunk_rays[wave][slot];
           pix = __float_as_uint(r.w);
           if (pix != kIdle) {
-            pix_tile = cur_tile;
+            pix_pos = cur_base + slot;
             pix_body0 = acc_body;
             d = mk(r.x, r.y, r.z);
             o = f.origin;
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
             need_point = true;
           }
         }
-        slots_used = min(kTile, slots_used + (uint32_t)__popcll(want));
+        slots_used = min(kChunk, slots_used + (uint32_t)__popcll(want));
       }
     }
 
@@ -303,6 +317,22 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     atomicAdd(a.debug + 1, (unsigned long long)n_service);
     atomicMin(a.debug + 3, (unsigned long long)stamp_real0);  // first wave start (100 MHz)
     atomicMax(a.debug + 4, (unsigned long long)__builtin_amdgcn_s_memrealtime());  // last wave end
+  }
+  {
+    const uint32_t w = blockIdx.x * 4u + wave;
+    uint32_t hw = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (lane == 0 && w < kWaveDebugSlots) {
+      unsigned long long* r = g_wave_debug + 8u * w;
+      r[0] = n_loop;
+      r[1] = n_body;
+      r[2] = n_service;
+      r[3] = stamp_service;
+      r[4] = __builtin_amdgcn_s_memtime() - stamp_begin;
+      r[5] = stamp_real0;
+      r[6] = real_exhaust;
+      r[7] = ((unsigned long long)hw << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - stamp_real0);
+    }
   }
 #endif
   if (lane == 0) {
@@ -431,10 +461,14 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS>, 256, 0);
     if (e != hipSuccess) return e;
     blocks_per_cu = n > 0 ? n : 1;
+    if (const char* env = getenv("FRM_BLOCKS_PER_CU")) {  // experiments
+      const int v = atoi(env);
+      if (v >= 1 && v <= 16) blocks_per_cu = v;
+    }
   }
-  // every wave starts with one 8x8 tile; never launch more waves than tiles
+  // every wave starts with one chunk of 64 pixels; never launch more waves than chunks
   uint32_t blocks = (uint32_t)(blocks_per_cu * cu_count);
-  const uint32_t max_blocks = (args.tiles_total + 3u) / 4u;
+  const uint32_t max_blocks = ((args.npix + kChunk - 1u) / kChunk + 3u) / 4u;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) blocks = 1;
   hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(256), 0, stream, args);
@@ -484,3 +518,10 @@ hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst
 }
 
 }  // namespace frm
+
+#ifdef FRM_STAMPS
+extern "C" int frm_debug_waves(uint64_t* out, size_t slots) {
+  if (slots > frm::kWaveDebugSlots) slots = frm::kWaveDebugSlots;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(frm::g_wave_debug), slots * 64) == hipSuccess ? (int)slots : -1;
+}
+#endif

@@ -29,12 +29,13 @@ try:
 except AttributeError:
     pass
 try:
-    tiles = ((w.width + 7) // 8) * ((w.height + 7) // 8)
-    costs = np.zeros(tiles, np.uint32)
-    lib.frm_debug_tile_costs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
-    n = lib.frm_debug_tile_costs(r.ctx, costs.ctypes.data, tiles)
-    c = np.sort(costs[:n])[::-1]
-    print("per-tile max bodies/pixel: max", c[0], "p99.9", c[int(n*0.001)], "p99", c[int(n*0.01)], "p90", c[int(n*0.1)], "median", c[n//2])
-    print("tiles with cost >= half max:", int((c >= c[0] / 2).sum()), "of", n)
+    npix = w.width * w.height
+    keys = np.zeros(npix, np.uint8)
+    lib.frm_debug_pixel_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    n = lib.frm_debug_pixel_keys(r.ctx, keys.ctypes.data, npix)
+    bodies = np.sort(np.exp2(keys[:n] / 16.0) - 1.0)[::-1]  # key -> approx. bodies per pixel
+    print("per-pixel bodies (from keys): max", int(bodies[0]), "p99.9", int(bodies[int(n * 0.001)]),
+          "p99", int(bodies[int(n * 0.01)]), "p90", int(bodies[int(n * 0.1)]), "median", int(bodies[n // 2]))
+    print("share of all bodies in the top 1% of pixels:", round(float(bodies[: n // 100].sum() / bodies.sum()), 3))
 except AttributeError:
     pass
