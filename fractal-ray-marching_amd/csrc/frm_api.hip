@@ -20,7 +20,7 @@ using namespace frm;
 
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
-static constexpr uint32_t kDefaultServiceMin = 28;  // swept 12..32 on MI355X (round 1)
+static constexpr uint32_t kDefaultServiceMin = 24;  // swept 16..36 on MI355X (round 1): flat 16-28
 
 struct frm_ctx {
   int device = 0;
@@ -35,14 +35,13 @@ struct frm_ctx {
   unsigned int* queue = nullptr;
   ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
   size_t records_cap = 0;
-  // pixel scheduling state (frm_sched.hip), sched_cap entries each: two fetch orders
-  // (the last launch's and the next), the cost keys the last launch recorded per fetch
-  // position, the sort's key output; plus the sort's temp space
-  uint32_t* sched_order[2] = {nullptr, nullptr};
+  // pixel scheduling state (frm_sched.hip), sched_cap entries each: 0..cap-1, the fetch
+  // order, the cost keys the last launch recorded per pixel and the sort's key output
+  uint32_t* sched_iota = nullptr;
+  uint32_t* sched_order = nullptr;
   uint8_t* sched_keys = nullptr;  // 2 x sched_cap: keys, sorted keys
   void* sched_temp = nullptr;
   size_t sched_cap = 0, sched_temp_bytes = 0;
-  int sched_cur = 0;       // sched_order[sched_cur] is the last launch's order
   uint64_t sched_key = 0;  // geometry the recorded keys belong to
   bool sched_history = false;
   uint32_t service_min = kDefaultServiceMin;
@@ -142,19 +141,18 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
     const uint32_t npix = a.npix;
     if (npix > ctx->sched_cap) {
       FRM_HIP(ctx, hipStreamSynchronize(s));
-      for (auto*& o : ctx->sched_order) {
-        if (o) FRM_HIP(ctx, hipFree(o));
-        o = nullptr;
-      }
-      if (ctx->sched_keys) FRM_HIP(ctx, hipFree(ctx->sched_keys));
-      if (ctx->sched_temp) FRM_HIP(ctx, hipFree(ctx->sched_temp));
+      for (void* b : {(void*)ctx->sched_iota, (void*)ctx->sched_order, (void*)ctx->sched_keys, ctx->sched_temp})
+        if (b) FRM_HIP(ctx, hipFree(b));
+      ctx->sched_iota = ctx->sched_order = nullptr;
       ctx->sched_keys = nullptr;
       ctx->sched_temp = nullptr;
       ctx->sched_cap = 0;
       ctx->sched_temp_bytes = schedule_temp_bytes(npix);
-      for (auto*& o : ctx->sched_order) FRM_HIP(ctx, hipMalloc(&o, (size_t)npix * sizeof(uint32_t)));
+      FRM_HIP(ctx, hipMalloc(&ctx->sched_iota, (size_t)npix * sizeof(uint32_t)));
+      FRM_HIP(ctx, hipMalloc(&ctx->sched_order, (size_t)npix * sizeof(uint32_t)));
       FRM_HIP(ctx, hipMalloc(&ctx->sched_keys, (size_t)npix * 2));
       FRM_HIP(ctx, hipMalloc(&ctx->sched_temp, ctx->sched_temp_bytes ? ctx->sched_temp_bytes : 16));
+      FRM_HIP(ctx, fill_iota(ctx->sched_iota, npix, s));
       ctx->sched_cap = npix;
       ctx->sched_history = false;
     }
@@ -162,12 +160,9 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
                          ((uint64_t)a.g.band_rows << 8) ^ ((uint64_t)a.g.first_band << 4) ^ a.g.band_stride ^
                          ((uint64_t)a.f.height << 52);
     const bool history = ctx->sched_history && key == ctx->sched_key;
-    const uint32_t* prev = ctx->sched_order[ctx->sched_cur];
-    uint32_t* next = ctx->sched_order[ctx->sched_cur ^ 1];
-    FRM_HIP(ctx, schedule_pixels(npix, history, ctx->sched_keys, ctx->sched_keys + ctx->sched_cap, prev, next,
-                                 ctx->sched_temp, ctx->sched_temp_bytes, s));
-    ctx->sched_cur ^= 1;
-    a.pixel_order = next;
+    FRM_HIP(ctx, schedule_pixels(npix, history, ctx->sched_keys, ctx->sched_keys + ctx->sched_cap,
+                                 ctx->sched_iota, ctx->sched_order, ctx->sched_temp, ctx->sched_temp_bytes, s));
+    a.pixel_order = ctx->sched_order;
     a.pixel_key = ctx->sched_keys;
     ctx->sched_key = key;
     ctx->sched_history = true;
@@ -252,9 +247,8 @@ int frm_destroy(frm_ctx* ctx) {
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->queue) (void)hipFree(ctx->queue);
   if (ctx->records) (void)hipFree(ctx->records);
-  for (uint32_t* o : ctx->sched_order)
-    if (o) (void)hipFree(o);
-  if (ctx->sched_keys) (void)hipFree(ctx->sched_keys);
+  for (void* b : {(void*)ctx->sched_iota, (void*)ctx->sched_order, (void*)ctx->sched_keys})
+    if (b) (void)hipFree(b);
   if (ctx->sched_temp) (void)hipFree(ctx->sched_temp);
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
@@ -386,7 +380,7 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
 extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
   return hipMemcpy(out5, ctx->queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
-// per-pixel cost keys recorded by the last persistent launch, by fetch position (before
+// per-pixel cost keys recorded by the last persistent launch (local pixel order; before
 // the next launch overwrites them)
 extern "C" int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
   if (n > ctx->sched_cap) n = ctx->sched_cap;

@@ -32,7 +32,7 @@ __device__ __forceinline__ float sqrt_nosmall(float x) {
   float r_up = fmaf(-s_up, s, x);
   s = (r_dn <= 0.0f) ? s_dn : s;
   s = (r_up > 0.0f) ? s_up : s;
-  return __builtin_amdgcn_class(x, 0x260) ? x : s;  // +-0 and +inf pass through
+  return __builtin_amdgcn_classf(x, 0x260) ? x : s;  // +-0 and +inf pass through (f32 class)
 }
 
 // Correctly rounded a / b for a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40].

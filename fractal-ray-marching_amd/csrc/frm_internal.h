@@ -33,7 +33,7 @@ struct KernelArgs {
   uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
   unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
   const uint32_t* pixel_order;    // persistent kernel: local pixel index at each fetch position
-  uint8_t* pixel_key;             // persistent kernel: cost key per fetch position (out)
+  uint8_t* pixel_key;             // persistent kernel: cost key per local pixel (out)
 };
 
 // frm_kernels.hip
@@ -42,12 +42,13 @@ hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, 
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,
                             uint32_t height, uint32_t band_rows, uint32_t ranks,
                             hipStream_t stream);
-// Pixel scheduling (frm_sched.hip). With history, next = prev reordered by descending
-// key[i] (the cost key the last launch recorded for the pixel it fetched at position i;
-// stable, one 8-bit radix pass); without, next = 0, 1, ..., npix - 1 (row-major).
+// Pixel scheduling (frm_sched.hip). With history, order = the local pixels 0..npix-1
+// (iota) by descending key[p], the cost key the last launch recorded for pixel p (stable,
+// one 8-bit radix pass); without, order = iota (row-major).
 hipError_t schedule_pixels(uint32_t npix, bool has_history, const uint8_t* key, uint8_t* key_sorted,
-                           const uint32_t* prev, uint32_t* next, void* temp, size_t temp_bytes,
+                           const uint32_t* iota, uint32_t* order, void* temp, size_t temp_bytes,
                            hipStream_t stream);
+hipError_t fill_iota(uint32_t* out, uint32_t n, hipStream_t stream);
 size_t schedule_temp_bytes(uint32_t npix);
 hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
                              hipStream_t stream);

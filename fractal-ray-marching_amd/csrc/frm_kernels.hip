@@ -117,9 +117,8 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
   v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
-  uint32_t acc_body = 0, acc_bail = 0;  // per-lane Mandelbulb work counters
-  uint32_t cur_base = 0;                 // wave-uniform: fetch position of the chunk's slot 0
-  uint32_t pix_pos = 0, pix_body0 = 0;   // per lane: fetch position of the pixel, bodies at its start
+  uint32_t acc_body = 0;   // per-lane Mandelbulb bodies
+  uint32_t pix_body0 = 0;  // acc_body when the lane's pixel started
 #ifdef FRM_STAMPS
   uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
   const uint64_t stamp_begin = __builtin_amdgcn_s_memtime();
@@ -156,14 +155,14 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
 #ifdef FRM_STAMPS  // diagnostic build: wave cycles spent in service passes -> counters[7]
     const uint64_t stamp0 = __builtin_amdgcn_s_memtime();
 #endif
-    bool ev_prim = false, ev_hit = false, ev_shadow = false;
+    bool ev_prim = false, ev_hit = false, ev_shadow = false, ev_bail = false;
     // 1. consume finished DEs: march / normal / shadow bookkeeping
     if (pix != kIdle && done) {
       done = false;
       if constexpr (FAM == kMandelbulb) {
         de = mb_distance(mag, dr);
-        acc_body += body;             // bodies this DE ran (N+1 on a count exit)
-        acc_bail += body <= n_iter;   // exits by bailout (incl. before the first body)
+        acc_body += body;          // bodies this DE ran (N+1 on a count exit)
+        ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
       }
       if (phase == kPrimary) {
         ev_prim = true;
@@ -179,7 +178,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
             need_point = true;
           } else {  // miss: BACKGROUND_COLOR
             rec[pix].flags = 0u;
-            a.pixel_key[pix_pos] = cost_key(acc_body - pix_body0);
+            a.pixel_key[pix] = cost_key(acc_body - pix_body0);
             pix = kIdle;
           }
         }
@@ -221,7 +220,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         if (finished) {
           *reinterpret_cast<uint4*>(&rec[pix].closeness) =
               make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u), 0u);
-          a.pixel_key[pix_pos] = cost_key(acc_body - pix_body0);
+          a.pixel_key[pix] = cost_key(acc_body - pix_body0);
           pix = kIdle;
         }
       }
@@ -253,7 +252,6 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           chunk_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
           __builtin_amdgcn_wave_barrier();
           slots_used = 0;
-          cur_base = base;
         }
       }
       if (slots_used < kChunk) {
@@ -262,7 +260,6 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           const float4 r = chunk_rays[wave][slot];
           pix = __float_as_uint(r.w);
           if (pix != kIdle) {
-            pix_pos = cur_base + slot;
             pix_body0 = acc_body;
             d = mk(r.x, r.y, r.z);
             o = f.origin;
@@ -298,6 +295,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     n_prim += count(ev_prim);
     n_hit += count(ev_hit);
     n_shadow += count(ev_shadow);
+    n_bail += count(ev_bail);
 #ifdef FRM_STAMPS
     stamp_service += __builtin_amdgcn_s_memtime() - stamp0;
     n_service++;
@@ -306,10 +304,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     if (exhausted && __ballot(pix != kIdle) == 0) break;
   }
 
-  if constexpr (FAM == kMandelbulb) {
-    n_body = wave_sum(acc_body);
-    n_bail = wave_sum(acc_bail);
-  }
+  if constexpr (FAM == kMandelbulb) n_body = wave_sum(acc_body);
 #ifdef FRM_STAMPS
   if (lane == 0) {
     atomicAdd(&a.counters[7], (unsigned long long)stamp_service);

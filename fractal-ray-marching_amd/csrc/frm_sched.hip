@@ -3,9 +3,9 @@
 // A pixel's march is strictly sequential (up to 2 x max_steps DEs of up to N+1 bodies),
 // so a frame cannot end before its longest pixel, and pixels still running when the work
 // queue drains decide the frame's tail. The kernel records for every pixel an 8-bit
-// log-scale key of its cost (Mandelbulb bodies, frm_kernels.hip cost_key) at the position
-// it was fetched from; the next launch of the same geometry fetches pixels in descending
-// key order (longest-processing-time-first list scheduling over all lanes of the GPU).
+// log-scale key of its cost (Mandelbulb bodies, frm_kernels.hip cost_key); the next launch
+// of the same geometry fetches pixels in descending key order (longest-processing-time-
+// first list scheduling over all lanes of the GPU).
 // The sort is stable and 8 bits wide: one radix pass over npix (key, pixel) pairs.
 // Ordering never changes a pixel's bytes — every pixel is computed by the same
 // deterministic function, whichever lane runs it and whenever.
@@ -28,14 +28,18 @@ size_t schedule_temp_bytes(uint32_t npix) {
   return bytes;
 }
 
+hipError_t fill_iota(uint32_t* out, uint32_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(iota_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, out, n);
+  return hipGetLastError();
+}
+
 hipError_t schedule_pixels(uint32_t npix, bool has_history, const uint8_t* key, uint8_t* key_sorted,
-                           const uint32_t* prev, uint32_t* next, void* temp, size_t temp_bytes,
+                           const uint32_t* iota, uint32_t* order, void* temp, size_t temp_bytes,
                            hipStream_t stream) {
   if (has_history)
-    return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key, key_sorted, prev, next, (int)npix,
+    return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key, key_sorted, iota, order, (int)npix,
                                                         0, 8, stream);
-  hipLaunchKernelGGL(iota_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, stream, next, npix);
-  return hipGetLastError();
+  return hipMemcpyAsync(order, iota, (size_t)npix * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
 }
 
 }  // namespace frm

@@ -32,7 +32,7 @@ for k in range(3):
     ms = e0.elapsed_time(e1)
 lib = frm.load()
 lib.frm_debug_waves.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-raw = np.zeros((16384, 8), np.uint64)
+raw = np.zeros((16384, 16), np.uint64)
 n = lib.frm_debug_waves(raw.ctypes.data, 16384)
 rec = raw[:n]
 rec = rec[rec[:, 4] > 0]
@@ -48,6 +48,10 @@ print(f"body-loop lane utilisation {bodies.sum() / (64 * loops.sum()):.3f}; "
 print(f"service share of wave cycles {scyc.sum() / tcyc.sum():.3f}; service passes per wave {nserv.mean():.0f}; "
       f"body iterations per service pass {loops.sum() / nserv.sum():.2f}; cycles per pass {scyc.sum() / nserv.sum():.0f}; "
       f"cycles per body iteration {(tcyc.sum() - scyc.sum()) / loops.sum():.0f}")
+cons, refl, nfetch = (rec[:, i].astype(np.float64) for i in (8, 9, 10))
+print(f"service pass cycles: consume {cons.sum() / nserv.sum():.0f}, refill {refl.sum() / nserv.sum():.0f}, "
+      f"start-DE+counters {(scyc.sum() - cons.sum() - refl.sum()) / nserv.sum():.0f}; "
+      f"fetches per wave {nfetch.mean():.1f}")
 print(f"wave start spread {st.max():.0f} us; first exhaust {np.nanmin(ex):.0f} us, median exhaust {np.nanmedian(ex):.0f} us")
 q = np.percentile(en, [0, 10, 50, 90, 99, 100])
 print("wave end percentiles (us): " + " ".join(f"p{p_}={v:.0f}" for p_, v in zip([0, 10, 50, 90, 99, 100], q)))
