@@ -23,7 +23,9 @@ namespace frm {
 #if defined(__HIP_DEVICE_COMPILE__)
 
 // Correctly rounded sqrt, exact for x == +-0, x >= 2^-96, +inf, NaN and x < 0 (all x
-// except subnormals and normals below 2^-96). Mirrors LLVM's expansion minus the rescale.
+// except subnormals and normals below 2^-96). Mirrors LLVM's expansion minus the rescale
+// and minus its +-0/+inf pass-through: there the one-ulp corrections cannot fire
+// (s = +-0: s_dn is NaN, the s_up residual is +-0; s = +inf: both residuals are NaN).
 __device__ __forceinline__ float sqrt_nosmall(float x) {
   float s = __builtin_amdgcn_sqrtf(x);
   float s_dn = __uint_as_float(__float_as_uint(s) - 1u);
@@ -31,8 +33,7 @@ __device__ __forceinline__ float sqrt_nosmall(float x) {
   float r_dn = fmaf(-s_dn, s, x);
   float r_up = fmaf(-s_up, s, x);
   s = (r_dn <= 0.0f) ? s_dn : s;
-  s = (r_up > 0.0f) ? s_up : s;
-  return __builtin_amdgcn_classf(x, 0x260) ? x : s;  // +-0 and +inf pass through (f32 class)
+  return (r_up > 0.0f) ? s_up : s;
 }
 
 // Correctly rounded a / b for a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40].
@@ -47,6 +48,40 @@ __device__ __forceinline__ float div_tame(float a, float b) {
   q = fmaf(rem, r, q);
   const float zero = __uint_as_float((__float_as_uint(a) ^ __float_as_uint(b)) & 0x80000000u);
   return (a == 0.0f) ? zero : q;
+}
+
+// div_tame without the zero-numerator fix-up: for a = +0 the Newton sequence already
+// gives +0; for a = -0 it gives +0 where a / b is -0. Used where that sign cannot matter
+// (acos_dev(+-0) and atan2's min/max ratio, whose numerator is never -0).
+__device__ __forceinline__ float div_tame_nz(float a, float b) {
+  float r = __builtin_amdgcn_rcpf(b);
+  float e = fmaf(-b, r, 1.0f);
+  r = fmaf(e, r, r);
+  float q = a * r;
+  float rem = fmaf(-b, q, a);
+  q = fmaf(rem, r, q);
+  rem = fmaf(-b, q, a);
+  return fmaf(rem, r, q);
+}
+
+// sincos_ for finite |x| <= 2^22 * pi/2 (the quadrant clamp is a no-op there); negating through
+// the sign bit: (q & 2) ? -v : v == v ^ (bit 1 of q moved to bit 31). Bit-identical.
+__device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
+  float j = rintf(x * kTwoOverPi);
+  float r = fma_(-j, kHalfPi, x);
+  r = fma_(-j, kHalfPiLo, r);
+  const uint32_t q = (uint32_t)(int)j;
+  float z = r * r;
+  float ps = fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  float s = fma_(r * z, ps, r);
+  float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                  4.166664568298827e-2f);
+  float c = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
+  const bool odd = (q & 1u) != 0u;
+  float sv = odd ? c : s;
+  float cv = odd ? s : c;
+  *s_out = __uint_as_float(__float_as_uint(sv) ^ ((q << 30) & 0x80000000u));
+  *c_out = __uint_as_float(__float_as_uint(cv) ^ (((q + 1u) << 30) & 0x80000000u));
 }
 
 // acos_ with the exact-for-its-range sqrt (zb is 0 or >= 2^-25 for |t| <= 1; NaN/negative
@@ -69,7 +104,7 @@ __device__ __forceinline__ float acos_dev(float t) {
 __device__ __forceinline__ float atan2_tame(float y, float x) {
   float ax = fabsf(x), ay = fabsf(y);
   float mx = max_(ax, ay), mn = min_(ax, ay);
-  float a = div_tame(mn, mx);
+  float a = div_tame_nz(mn, mx);  // mn >= +0
   a = (mx == 0.0f) ? 0.0f : a;
   float s = a * a;
   float q = fma_(fma_(fma_(fma_(fma_(fma_(fma_(0.002974590389872539f, s, -0.016581183968493302f), s,

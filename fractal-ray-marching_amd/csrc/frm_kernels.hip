@@ -75,7 +75,7 @@ constexpr uint32_t kChunk = 64u;  // pixels per queue fetch (one per lane of the
 enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(__ballot(c)); }
+__device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(ballot(c)); }
 
 // Scheduling key of a finished pixel: 16 x log2(Mandelbulb bodies + 1), 0..255 (~4.4 %
 // steps). Only orders the next frame's fetches; never touches a pixel's bytes.
@@ -131,8 +131,8 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     // or no lane computes. The service pass costs the same however many lanes take part.
     if constexpr (FAM == kMandelbulb) {
       for (;;) {
-        const uint64_t busy = __ballot(pix != kIdle && !done);
-        const uint32_t waiting = exhausted ? (uint32_t)__popcll(__ballot(pix != kIdle && done))
+        const uint64_t busy = ballot(pix != kIdle && !done);
+        const uint32_t waiting = exhausted ? (uint32_t)__popcll(ballot(pix != kIdle && done))
                                            : 64u - (uint32_t)__popcll(busy);
         if (busy == 0 || waiting >= a.service_min) break;
 #ifdef FRM_STAMPS
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
       }
     }
     // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
-    const uint64_t want = __ballot(pix == kIdle);
+    const uint64_t want = ballot(pix == kIdle);
     if (want != 0 && !exhausted) {
       if (slots_used == kChunk) {
         uint32_t base = 0;
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     n_service++;
 #endif
 
-    if (exhausted && __ballot(pix != kIdle) == 0) break;
+    if (exhausted && ballot(pix != kIdle) == 0) break;
   }
 
   if constexpr (FAM == kMandelbulb) n_body = wave_sum(acc_body);
@@ -412,7 +412,20 @@ __global__ __launch_bounds__(256) void eval_math(int fn, const float* a, const f
     case 6: r = exp2_(x); break;
     case 7: r = pow_(x, y); break;
     case 8: r = sqrt_(x); break;
-    default: r = x / y; break;
+    case 9: r = x / y; break;
+#if defined(__HIP_DEVICE_COMPILE__)  // frm_fast.h is device-only
+    case 10: r = sqrt_nosmall(x); break;
+    case 11: r = div_tame(x, y); break;
+    case 12: r = div_tame_nz(x, y); break;
+    case 13: { float c; sincos_small(x, &r, &c); } break;
+    case 14: { float s; sincos_small(x, &s, &r); } break;
+    case 15: r = acos_dev(x); break;
+    case 16: r = atan2_tame(x, y); break;
+    case 17: r = log2_tame(x); break;
+    default: r = exp2_tame(x); break;
+#else
+    default: r = x; break;
+#endif
   }
   out[i] = r;
 }

@@ -189,27 +189,43 @@ FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 // distance = 0.5 * log(magnitude) * magnitude / magnitude_derivative, fragment.wgsl:269
 FRM_HD float mb_distance(float r, float dr) { return ((0.5f * log_(r)) * r) / dr; }
 
+#if defined(__HIPCC__)
+// Lane mask of a per-lane predicate (no int round trip, unlike HIP's __ballot(int)).
+__device__ __forceinline__ uint64_t ballot(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ballot_w64(b);
+#else
+  return b;
+#endif
+}
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // Operands of one Mandelbulb body are tame when r = length(z) is in [2^-40, bailout]
 // and every component of z is 0 or has magnitude >= 2^-60: then z.z / r and
 // min/max(|x|,|y|) are tame divisions, log2(r) has a positive normal argument and both
 // exp2 arguments ((P-1)*log2 r, P*log2 r with P <= 9) lie in [-400, 128].
-__device__ __forceinline__ bool comp_tame(float v) { return v == 0.0f || fabsf(v) >= 0x1p-60f; }
+// Branch-free: (bits << 1) - 1 drops the sign and maps +-0 to UINT_MAX, so one unsigned
+// min3 + compare tests "0 or |v| >= 2^-60" for the three components at once (NaN
+// components also pass, but then r is NaN and fails r >= 2^-40).
+__device__ __forceinline__ uint32_t comp_key(float v) { return (__float_as_uint(v) << 1) - 1u; }
 __device__ __forceinline__ bool mb_tame(v3 z, float r) {
-  return r >= 0x1p-40f && comp_tame(z.x) && comp_tame(z.y) && comp_tame(z.z);
+  constexpr uint32_t kMin = (0x21800000u << 1) - 1u;  // comp_key(0x1p-60f)
+  const uint32_t m = min(min(comp_key(z.x), comp_key(z.y)), comp_key(z.z));  // v_min3_u32
+  return (r >= 0x1p-40f) & (m >= kMin);
 }
 
 // mb_body (frm_scene.h) with the tame primitives: the same operations in the same order.
 __device__ __forceinline__ void mb_body_tame(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
   const float P = u.mb_power, Pm1 = u.mb_power_m1;
-  float theta = acos_dev(div_tame(z.z, r));
+  float theta = acos_dev(div_tame_nz(z.z, r));  // acos_dev(-0) == acos_dev(+0)
   float phi = atan2_tame(z.y, z.x);
   float l2 = log2_tame(r);
   dr = fma_(exp2_tame(Pm1 * l2) * P, dr, 1.0f);
   float er = exp2_tame(P * l2);
   float st, ct, sp, cp;
-  sincos_(theta * P, &st, &ct);
-  sincos_(phi * P, &sp, &cp);
+  sincos_small(theta * P, &st, &ct);  // |theta * P|, |phi * P| <= 9 pi (P in [4, 9])
+  sincos_small(phi * P, &sp, &cp);
   z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
 }
 
@@ -226,7 +242,7 @@ __device__ __forceinline__ bool length_small(v3 a) {
 // its active lanes have tame operands. Bit-identical to mb_body either way.
 FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (__ballot(!mb_tame(z, r)) == 0) {
+  if (ballot(!mb_tame(z, r)) == 0) {
     mb_body_tame(u, c, r, z, dr);
     return;
   }
@@ -236,7 +252,7 @@ FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 // length(z) for the Mandelbulb magnitude; fast sqrt unless a lane has 0 < |z|^2 < 2^-96.
 FRM_HD float mb_length(v3 z) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (__ballot(length_small(z)) == 0) return length_nosmall(z);
+  if (ballot(length_small(z)) == 0) return length_nosmall(z);
 #endif
   return length(z);
 }

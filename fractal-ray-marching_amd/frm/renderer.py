@@ -78,7 +78,11 @@ class Renderer:
 
     # diagnostics: scene() and builtins evaluated on the GPU
     MATH_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "log": 4, "log2": 5, "exp2": 6,
-               "pow": 7, "sqrt": 8, "div": 9}
+               "pow": 7, "sqrt": 8, "div": 9,
+               # device fast paths (frm_fast.h), each bit-identical to a builtin on its domain
+               "sqrt_nosmall": 10, "div_tame": 11, "div_tame_nz": 12, "sin_small": 13,
+               "cos_small": 14, "acos_dev": 15, "atan2_tame": 16, "log2_tame": 17,
+               "exp2_tame": 18}
 
     def eval_scene(self, points):
         pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)

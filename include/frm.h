@@ -166,7 +166,12 @@ int frm_stats_from_counters(const frm_ctx* ctx, const uint64_t* counters, frm_st
 enum {
   FRM_MATH_SIN = 0, FRM_MATH_COS = 1, FRM_MATH_ACOS = 2, FRM_MATH_ATAN2 = 3,
   FRM_MATH_LOG = 4, FRM_MATH_LOG2 = 5, FRM_MATH_EXP2 = 6, FRM_MATH_POW = 7,
-  FRM_MATH_SQRT = 8, FRM_MATH_DIV = 9
+  FRM_MATH_SQRT = 8, FRM_MATH_DIV = 9,
+  /* device fast paths (bit-identical to the builtin above on their stated domain, used by
+     the Mandelbulb body when a whole wave qualifies; csrc/frm_fast.h) */
+  FRM_MATH_SQRT_NOSMALL = 10, FRM_MATH_DIV_TAME = 11, FRM_MATH_DIV_TAME_NZ = 12,
+  FRM_MATH_SIN_SMALL = 13, FRM_MATH_COS_SMALL = 14, FRM_MATH_ACOS_DEV = 15,
+  FRM_MATH_ATAN2_TAME = 16, FRM_MATH_LOG2_TAME = 17, FRM_MATH_EXP2_TAME = 18
 };
 int frm_eval_scene(frm_ctx* ctx, const float* points, uint32_t n, float* out_distance,
                    float* out_color);

@@ -90,3 +90,68 @@ def test_mandelbulb_tame_and_exact_paths(gpu_renderer_factory, oracle):
                 d, col = r.eval_scene(pts)
                 rd, rcol, _ = oracle.scene_de(p, pts)
                 assert same_bits(d, rd), f"N={iters}: {np.sum(~((d.view(np.uint32) == rd.view(np.uint32)) | (np.isnan(d) & np.isnan(rd))))} mismatches"
+
+
+def _tame(rng, n, lo=-60, hi=40, zeros=True):
+    """Values 0 (if zeros) or +-2^e * mantissa with e in [lo, hi): the tame operand range."""
+    mag = np.clip(np.exp2(rng.uniform(lo, hi, n)), 2.0 ** lo, 2.0 ** hi)
+    v = (mag * rng.choice([-1.0, 1.0], n)).astype(np.float32)
+    if zeros:
+        v[rng.random(n) < 0.02] = 0.0
+    return v
+
+
+def _fast_inputs(name, rng):
+    n = 200000
+    if name == "sqrt_nosmall":
+        a = np.concatenate([np.exp2(rng.uniform(-96, 128, n)), [0.0, -0.0, np.inf, -1.0, np.nan, 2.0 ** -96,
+                                                                np.finfo(np.float32).max, 1.0]])
+        return "sqrt", a, None
+    if name in ("div_tame", "div_tame_nz"):
+        a, b = _tame(rng, n), _tame(rng, n, zeros=False)
+        if name == "div_tame":
+            a = np.concatenate([a, [0.0, -0.0, -0.0, 2.0 ** -60, 2.0 ** 40]])
+            b = np.concatenate([b, [-3.0, 5.0, -5.0, 2.0 ** 40, 2.0 ** -60]])
+        else:  # the numerator is never -0 there (frm_fast.h)
+            a[a == 0] = 0.0
+        return "div", a, b
+    if name in ("sin_small", "cos_small"):
+        lim = 2.0 ** 22 * np.pi / 2 * 0.999
+        a = np.concatenate([rng.uniform(-30, 30, n), rng.uniform(-lim, lim, n // 4),
+                            [0.0, -0.0, np.pi, -np.pi, 9 * np.pi, lim, -lim]])
+        return name.split("_")[0], a, None
+    if name == "acos_dev":
+        return "acos", np.concatenate([rng.uniform(-1, 1, n), [1, -1, 0.5, -0.5, 0.0, -0.0, 1.0000001, np.nan]]), None
+    if name == "atan2_tame":
+        return "atan2", _tame(rng, n), _tame(rng, n)
+    if name == "log2_tame":
+        return "log2", np.concatenate([np.exp2(rng.uniform(-126, 128, n)), [1.0, 2.0 ** -126, 0.7071067]]), None
+    # exp2_tame: finite y in [-400, 128]
+    a = np.concatenate([rng.uniform(-400, 128, n), rng.uniform(-1, 1, 1000), np.arange(-150, 129), [-400.0, 127.999]])
+    return "exp2", a, None
+
+
+FAST = ["sqrt_nosmall", "div_tame", "div_tame_nz", "sin_small", "cos_small", "acos_dev", "atan2_tame",
+        "log2_tame", "exp2_tame"]
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_fast_path_bit_exact_on_its_domain(gpu, oracle, name):
+    """Each device fast path (frm_fast.h) equals the exact builtin bit for bit on the operand
+    domain the tame Mandelbulb body guarantees for it."""
+    rng = np.random.default_rng(11)
+    ref_name, a, b = _fast_inputs(name, rng)
+    a = a.astype(np.float32)
+    b = None if b is None else b.astype(np.float32)
+    got = gpu.eval_math(name, a, b)
+    ref = oracle.math_fn(ref_name, a, b)
+    bad = ~((got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref)))
+    assert not bad.any(), f"{name}: {bad.sum()} mismatches, e.g. a={a[bad][:3]} gpu={got[bad][:3]} cpu={ref[bad][:3]}"
+
+
+def test_div_tame_nz_zero_numerator_sign(gpu):
+    """The documented difference: -0 / b gives +0 (acos_dev(+-0) agree, so it cannot matter)."""
+    got = gpu.eval_math("div_tame_nz", np.array([-0.0, 0.0], np.float32), np.array([2.0, -2.0], np.float32))
+    assert got.view(np.uint32).tolist() == [0, 0x80000000]  # -0/2 -> +0 (exact: -0); +0/-2 -> -0
+    assert gpu.eval_math("acos_dev", np.array([-0.0], np.float32)).view(np.uint32)[0] == \
+        gpu.eval_math("acos_dev", np.array([0.0], np.float32)).view(np.uint32)[0]
