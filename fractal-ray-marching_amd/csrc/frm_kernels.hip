@@ -84,9 +84,9 @@ __device__ __forceinline__ uint8_t cost_key(uint32_t bodies) {
 }
 
 #ifdef FRM_STAMPS
-// diagnostic build: one 8 x u64 record per wave of the last persistent launch
+// diagnostic build: one 16 x u64 record per wave of the last persistent launch
 constexpr uint32_t kWaveDebugSlots = 16384u;
-__device__ unsigned long long g_wave_debug[8u * kWaveDebugSlots];
+__device__ unsigned long long g_wave_debug[16u * kWaveDebugSlots];
 #endif
 
 template <uint32_t FAM, bool ITERS>
@@ -121,6 +121,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
   uint32_t pix_body0 = 0;  // acc_body when the lane's pixel started
 #ifdef FRM_STAMPS
   uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
+  uint64_t stamp_consume = 0, stamp_refill = 0, n_fetch = 0;
   const uint64_t stamp_begin = __builtin_amdgcn_s_memtime();
   const uint64_t stamp_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -226,12 +227,19 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
       }
     }
     // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
+#ifdef FRM_STAMPS
+    const uint64_t stamp1 = __builtin_amdgcn_s_memtime();
+    stamp_consume += stamp1 - stamp0;
+#endif
     const uint64_t want = ballot(pix == kIdle);
     if (want != 0 && !exhausted) {
       if (slots_used == kChunk) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(a.queue, kChunk);
         base = uniform(__shfl(base, 0, 64));
+#ifdef FRM_STAMPS
+        n_fetch++;
+#endif
         if (base >= total) {
           exhausted = true;
 #ifdef FRM_STAMPS
@@ -273,6 +281,9 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
       }
     }
 
+#ifdef FRM_STAMPS
+    stamp_refill += __builtin_amdgcn_s_memtime() - stamp1;
+#endif
     // 3. start the next DE of every lane that needs one (the hit point of the normal
     //    taps is recomputed from the unchanged primary ray: ray_at(o, t_hit, d))
     if (need_point) {
@@ -318,7 +329,10 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     uint32_t hw = 0;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     if (lane == 0 && w < kWaveDebugSlots) {
-      unsigned long long* r = g_wave_debug + 8u * w;
+      unsigned long long* r = g_wave_debug + 16u * w;
+      r[8] = stamp_consume;
+      r[9] = stamp_refill;
+      r[10] = n_fetch;
       r[0] = n_loop;
       r[1] = n_body;
       r[2] = n_service;
@@ -530,6 +544,6 @@ hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst
 #ifdef FRM_STAMPS
 extern "C" int frm_debug_waves(uint64_t* out, size_t slots) {
   if (slots > frm::kWaveDebugSlots) slots = frm::kWaveDebugSlots;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(frm::g_wave_debug), slots * 64) == hipSuccess ? (int)slots : -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(frm::g_wave_debug), slots * 128) == hipSuccess ? (int)slots : -1;
 }
 #endif
