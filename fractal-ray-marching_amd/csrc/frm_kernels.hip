@@ -122,8 +122,14 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
 #ifdef FRM_STAMPS
   uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
   uint64_t stamp_consume = 0, stamp_refill = 0, n_fetch = 0;
+  uint64_t stamp_sub[4] = {0, 0, 0, 0};  // consume: distance, primary, taps, shadow
   const uint64_t stamp_begin = __builtin_amdgcn_s_memtime();
   const uint64_t stamp_real0 = __builtin_amdgcn_s_memrealtime();
+#define FRM_SUB_BEGIN() const uint64_t sub0 = __builtin_amdgcn_s_memtime()
+#define FRM_SUB_END(k) stamp_sub[k] += __builtin_amdgcn_s_memtime() - sub0
+#else
+#define FRM_SUB_BEGIN()
+#define FRM_SUB_END(k)
 #endif
 
   for (;;) {
@@ -161,11 +167,14 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     if (pix != kIdle && done) {
       done = false;
       if constexpr (FAM == kMandelbulb) {
+        FRM_SUB_BEGIN();
         de = mb_distance(mag, dr);
         acc_body += body;          // bodies this DE ran (N+1 on a count exit)
         ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
+        FRM_SUB_END(0);
       }
       if (phase == kPrimary) {
+        FRM_SUB_BEGIN();
         ev_prim = true;
         if (de <= kMinDistance) {  // hit: object_result.distance = t >= 0
           ev_hit = true;
@@ -183,7 +192,9 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
             pix = kIdle;
           }
         }
+        FRM_SUB_END(1);
       } else if (phase != kShadow) {  // normal taps k.xyy, k.yyx, k.yxy, k.xxx
+        FRM_SUB_BEGIN();
         if (phase == kTap0) nsum = mk(de, -de, -de);
         else if (phase == kTap0 + 1) nsum = mk(nsum.x - de, nsum.y - de, nsum.z + de);
         else if (phase == kTap0 + 2) nsum = mk(nsum.x - de, nsum.y + de, nsum.z - de);
@@ -202,7 +213,9 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           phase++;
         }
         need_point = true;
+        FRM_SUB_END(2);
       } else {  // shadow march toward the sun
+        FRM_SUB_BEGIN();
         ev_shadow = true;
         closeness = min_(closeness, de / t);
         bool finished = false, sun_miss = false;
@@ -224,6 +237,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           a.pixel_key[pix] = cost_key(acc_body - pix_body0);
           pix = kIdle;
         }
+        FRM_SUB_END(3);
       }
     }
     // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
@@ -333,6 +347,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
       r[8] = stamp_consume;
       r[9] = stamp_refill;
       r[10] = n_fetch;
+      for (int k = 0; k < 4; ++k) r[11 + k] = stamp_sub[k];
       r[0] = n_loop;
       r[1] = n_body;
       r[2] = n_service;

@@ -52,6 +52,8 @@ cons, refl, nfetch = (rec[:, i].astype(np.float64) for i in (8, 9, 10))
 print(f"service pass cycles: consume {cons.sum() / nserv.sum():.0f}, refill {refl.sum() / nserv.sum():.0f}, "
       f"start-DE+counters {(scyc.sum() - cons.sum() - refl.sum()) / nserv.sum():.0f}; "
       f"fetches per wave {nfetch.mean():.1f}")
+sub = [rec[:, 11 + k].astype(np.float64).sum() / nserv.sum() for k in range(4)]
+print("consume sub-blocks, cycles per pass: distance %.0f, primary %.0f, taps %.0f, shadow %.0f" % tuple(sub))
 print(f"wave start spread {st.max():.0f} us; first exhaust {np.nanmin(ex):.0f} us, median exhaust {np.nanmedian(ex):.0f} us")
 q = np.percentile(en, [0, 10, 50, 90, 99, 100])
 print("wave end percentiles (us): " + " ".join(f"p{p_}={v:.0f}" for p_, v in zip([0, 10, 50, 90, 99, 100], q)))
