@@ -46,28 +46,31 @@ def parse():
 
 
 def cpu_baseline(params, w, seconds):
-    """Oracle (C restatement, thread pool with a dynamic row queue) on a bounded,
-    evenly spaced row sample of the same frame; steps/s extrapolates per step."""
+    """Oracle (C restatement, thread pool with a dynamic row queue) on a bounded, evenly
+    spaced row sample of the same frame, sized to about `seconds` of CPU work; steps/s
+    extrapolates per march step."""
     from oracle import frm_oracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
     flags = 1 if w.sphere else 0
-    # calibration: 8 evenly spaced rows
-    stride = max(1, w.height // 8)
-    rows = list(range(stride // 2, w.height, stride))
-    t0 = time.perf_counter()
-    r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows, threads=threads)
-    dt = time.perf_counter() - t0
-    per_row = dt / len(rows)
-    n = int(max(len(rows), min(w.height, seconds / max(per_row, 1e-9))))
-    if n > len(rows):
-        stride = max(1, w.height // n)
+
+    def sample(n):
+        stride = max(1, w.height // max(1, n))
         rows = list(range(stride // 2, w.height, stride))
         t0 = time.perf_counter()
-        r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows,
-                              threads=threads)
-        dt = time.perf_counter() - t0
+        r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows, threads=threads)
+        return rows, stride, r, time.perf_counter() - t0
+
+    # calibrate with >= 2 rows per thread (fewer rows than threads would time the slowest
+    # row, not the pool), then size the sample to the target, twice at most
+    n = min(w.height, 2 * threads)
+    rows, stride, r, dt = sample(n)
+    for _ in range(2):
+        if dt >= 0.6 * seconds or len(rows) >= w.height:
+            break
+        n = min(w.height, int(len(rows) * seconds / max(dt, 1e-3)))
+        rows, stride, r, dt = sample(n)
     c = r["counters"]
     steps = int(c[2]) + int(c[3])
     return {
@@ -79,6 +82,20 @@ def cpu_baseline(params, w, seconds):
                   f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O2, {threads} threads",
         "frames_per_s_extrapolated": (len(rows) / w.height) / dt,
     }
+
+
+def pmc_traffic(workload, world):
+    """HBM bytes per launch of the dominant kernel (march_persistent) from the committed
+    rocprofv3 --pmc passes of this workload (tools/pmc.sh + tools/pmc_summary.py: separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled and KiB -> B per
+    MI355X_MICROARCH.md). PMC collection needs its own profiler passes, so bench.py reports
+    the committed measurement and names it; None when there is none for this workload."""
+    path = os.path.join(ROOT, "profiles", "round1", f"pmc_{workload}_march.json")
+    if world != 1 or not os.path.exists(path):
+        return None, None
+    with open(path) as fh:
+        s = json.load(fh)
+    return s["hbm_read_bytes"] + s["hbm_write_bytes"], os.path.relpath(path, ROOT)
 
 
 def main():
@@ -162,6 +179,7 @@ def main():
         avg_kernel_s = kernel_ms / 1e3 / args.steps
         wom_per_launch = st["wom_ops"] / args.steps / world
         achieved = wom_per_launch / avg_kernel_s / 1e12
+        traffic, traffic_src = pmc_traffic(args.workload, world)
         out = {
             "metric": METRIC,
             "value": steps_total / elapsed / 1e9,
@@ -190,7 +208,8 @@ def main():
                 "peak": VALU_PEAK_TOPS,
                 "unit": "Tlane-op/s",
                 "frac": achieved / VALU_PEAK_TOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "frm::render",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_ops_per_launch": wom_per_launch,

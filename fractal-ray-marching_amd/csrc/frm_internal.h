@@ -17,7 +17,7 @@ struct ShadeRecord {
   float closeness;          // shadow march closeness
   uint32_t psteps;          // primary march steps (ambient occlusion)
   uint32_t flags;           // kRecHit | kRecSunMiss; 0 = primary miss
-  uint32_t pad;
+  uint32_t key;             // scheduling cost key (frm_sched.hip); shade_pass copies it out
 };
 constexpr uint32_t kRecHit = 1u, kRecSunMiss = 2u;
 

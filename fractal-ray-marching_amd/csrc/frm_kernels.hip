@@ -187,8 +187,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
           if (it < f.max_steps && t < kMaxTotalDistance) {
             need_point = true;
           } else {  // miss: BACKGROUND_COLOR
-            rec[pix].flags = 0u;
-            a.pixel_key[pix] = cost_key(acc_body - pix_body0);
+            *reinterpret_cast<uint2*>(&rec[pix].flags) = make_uint2(0u, cost_key(acc_body - pix_body0));
             pix = kIdle;
           }
         }
@@ -233,8 +232,8 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         }
         if (finished) {
           *reinterpret_cast<uint4*>(&rec[pix].closeness) =
-              make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u), 0u);
-          a.pixel_key[pix] = cost_key(acc_body - pix_body0);
+              make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u),
+                         cost_key(acc_body - pix_body0));
           pix = kIdle;
         }
         FRM_SUB_END(3);
@@ -381,6 +380,7 @@ __global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
   const uint32_t y = band_row_to_global(a.g, lr);
   if (y >= a.f.height) return;
   const uint4 r1 = *reinterpret_cast<const uint4*>(&a.records[idx].closeness);
+  if (a.pixel_key) a.pixel_key[idx] = (uint8_t)r1.w;  // coalesced, for the next frame's order
   uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
   if (r1.z & kRecHit) {
     const float4 r0 = *reinterpret_cast<const float4*>(&a.records[idx].t);
