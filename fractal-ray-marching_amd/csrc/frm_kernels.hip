@@ -77,8 +77,9 @@ enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(ballot(c)); }
 
-// Scheduling key of a finished pixel: 16 x log2(Mandelbulb bodies + 1), 0..255 (~4.4 %
-// steps). Only orders the next frame's fetches; never touches a pixel's bytes.
+// Scheduling key of a finished pixel: 16 x log2(cost + 1), 0..255 (~4.4 % steps); cost =
+// Mandelbulb bodies, or DE evaluations for the fixed-trip families. Only orders the next
+// frame's fetches; never touches a pixel's bytes.
 __device__ __forceinline__ uint8_t cost_key(uint32_t bodies) {
   return (uint8_t)min(255.0f, 16.0f * __log2f((float)bodies + 1.0f));
 }
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
   v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
-  uint32_t acc_body = 0;   // per-lane Mandelbulb bodies
+  uint32_t acc_body = 0;   // per-lane Mandelbulb bodies (other families: DEs, for scheduling)
   uint32_t pix_body0 = 0;  // acc_body when the lane's pixel started
 #ifdef FRM_STAMPS
   uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
@@ -313,6 +314,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         DeCount unused = {0u, 0u};
         de = scene_de<FAM, ITERS>(su, q, unused);
         done = true;
+        acc_body++;  // fixed-trip families: the scheduling cost unit is one DE
       }
     }
 
