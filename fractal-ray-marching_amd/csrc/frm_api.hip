@@ -20,7 +20,7 @@ using namespace frm;
 
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
-static constexpr uint32_t kDefaultServiceMin = 24;  // swept 16..36 on MI355X (round 1): flat 16-28
+static constexpr uint32_t kDefaultServiceMin = 20;  // swept 16..36 on MI355X (round 1): flat 16-24
 
 struct frm_ctx {
   int device = 0;

@@ -113,7 +113,6 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
   // per-lane state
   uint32_t pix = kIdle;      // local pixel index (lr * width + x) being marched
   uint32_t phase = kPrimary;
-  bool need_point = false;   // start a DE at the phase's next sample point
   bool done = false;         // the current DE has its result
   v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
@@ -163,9 +162,12 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
 #ifdef FRM_STAMPS  // diagnostic build: wave cycles spent in service passes -> counters[7]
     const uint64_t stamp0 = __builtin_amdgcn_s_memtime();
 #endif
-    bool ev_prim = false, ev_hit = false, ev_shadow = false, ev_bail = false;
-    // 1. consume finished DEs: march / normal / shadow bookkeeping
-    if (pix != kIdle && done) {
+    // 1. consume finished DEs. Branch-light: the bookkeeping of every phase is computed for
+    //    every lane with selects; only the distance, the last-tap transition (normal, record,
+    //    shadow ray) and the record store of a finished pixel are branches.
+    const bool cons = pix != kIdle && done;
+    bool ev_bail = false;
+    if (cons) {
       done = false;
       if constexpr (FAM == kMandelbulb) {
         FRM_SUB_BEGIN();
@@ -174,71 +176,53 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
         ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
         FRM_SUB_END(0);
       }
-      if (phase == kPrimary) {
-        FRM_SUB_BEGIN();
-        ev_prim = true;
-        if (de <= kMinDistance) {  // hit: object_result.distance = t >= 0
-          ev_hit = true;
-          psteps = it;
-          phase = kTap0;
-          need_point = true;
-        } else {
-          t = t + de;
-          it++;
-          if (it < f.max_steps && t < kMaxTotalDistance) {
-            need_point = true;
-          } else {  // miss: BACKGROUND_COLOR
-            *reinterpret_cast<uint2*>(&rec[pix].flags) = make_uint2(0u, cost_key(acc_body - pix_body0));
-            pix = kIdle;
-          }
-        }
-        FRM_SUB_END(1);
-      } else if (phase != kShadow) {  // normal taps k.xyy, k.yyx, k.yxy, k.xxx
-        FRM_SUB_BEGIN();
-        if (phase == kTap0) nsum = mk(de, -de, -de);
-        else if (phase == kTap0 + 1) nsum = mk(nsum.x - de, nsum.y - de, nsum.z + de);
-        else if (phase == kTap0 + 2) nsum = mk(nsum.x - de, nsum.y + de, nsum.z - de);
-        else nsum = mk(nsum.x + de, nsum.y + de, nsum.z + de);
-        if (phase == kTap3) {
-          const v3 n = normalize(nsum);
-          const v3 hp = ray_at(o, t, d);
-          *reinterpret_cast<float4*>(&rec[pix].t) = make_float4(t, n.x, n.y, n.z);
-          o = shadow_origin(hp, n);
-          d = to_sun();
-          t = 0.f;
-          it = 0;
-          closeness = kInfinity;
-          phase = kShadow;
-        } else {
-          phase++;
-        }
-        need_point = true;
-        FRM_SUB_END(2);
-      } else {  // shadow march toward the sun
-        FRM_SUB_BEGIN();
-        ev_shadow = true;
-        closeness = min_(closeness, de / t);
-        bool finished = false, sun_miss = false;
-        if (de <= kMinDistance) {
-          finished = true;
-        } else {
-          t = t + de;
-          it++;
-          if (it < f.max_steps && t < kMaxTotalDistance) {
-            need_point = true;
-          } else {
-            finished = true;
-            sun_miss = true;
-          }
-        }
-        if (finished) {
-          *reinterpret_cast<uint4*>(&rec[pix].closeness) =
-              make_uint4(__float_as_uint(closeness), psteps, kRecHit | (sun_miss ? kRecSunMiss : 0u),
-                         cost_key(acc_body - pix_body0));
-          pix = kIdle;
-        }
-        FRM_SUB_END(3);
-      }
+    }
+    const bool ev_prim = cons && phase == kPrimary, ev_shadow = cons && phase == kShadow;
+    const bool tap = cons && !ev_prim && !ev_shadow;  // normal taps k.xyy, k.yyx, k.yxy, k.xxx
+    const bool hit = de <= kMinDistance;              // object_result.distance >= 0
+    const bool ev_hit = ev_prim && hit;
+    // shadow closeness = min(closeness, d / t) before t moves (d / 0 on step 0, as in
+    // fragment.wgsl:292); computed by every lane, kept by shadow lanes
+    const float cl = min_(closeness, de / t);
+    closeness = ev_shadow ? cl : closeness;
+    const bool step = (ev_prim || ev_shadow) && !hit;  // march on: t += d, it++
+    const float t_next = t + de;
+    const uint32_t it_next = it + 1u;
+    const bool more = it_next < f.max_steps && t_next < kMaxTotalDistance;
+    t = step ? t_next : t;
+    it = step ? it_next : it;
+    psteps = ev_hit ? it : psteps;
+    const bool fin = (step && !more) || (ev_shadow && hit);  // primary miss, or shadow march ends
+    const bool sun_miss = ev_shadow && step && !more;
+    bool need_point = ev_hit || (step && more) || tap;  // start a DE at the phase's next sample point
+    // tap k adds s_k * d to the sum (k = 0 sets it); s_0..s_3 = (+--), (--+), (-+-), (+++)
+    const uint32_t k = phase - kTap0;
+    const float dx = (k == 0u || k == 3u) ? de : -de, dy = (k >= 2u) ? de : -de,
+                dz = (k == 1u || k == 3u) ? de : -de;
+    // (component-wise: a select of whole structs compiles to a select of stack addresses)
+    const float sx = (k == 0u) ? dx : nsum.x + dx, sy = (k == 0u) ? dy : nsum.y + dy,
+                sz = (k == 0u) ? dz : nsum.z + dz;
+    nsum = mk(tap ? sx : nsum.x, tap ? sy : nsum.y, tap ? sz : nsum.z);
+    phase = ev_hit ? kTap0 : (tap ? phase + 1u : phase);  // after the last tap: kShadow
+    if (tap && k == kTap3 - kTap0) {  // normal, then the shadow ray toward the sun
+      FRM_SUB_BEGIN();
+      const v3 n = normalize(nsum);
+      const v3 hp = ray_at(o, t, d);
+      *reinterpret_cast<float4*>(&rec[pix].t) = make_float4(t, n.x, n.y, n.z);
+      o = shadow_origin(hp, n);
+      d = to_sun();
+      t = 0.f;
+      it = 0;
+      closeness = kInfinity;
+      FRM_SUB_END(2);
+    }
+    if (fin) {  // primary miss (flags 0: BACKGROUND_COLOR) or end of the shadow march
+      FRM_SUB_BEGIN();
+      const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
+      *reinterpret_cast<uint4*>(&rec[pix].closeness) =
+          make_uint4(__float_as_uint(closeness), psteps, flags, cost_key(acc_body - pix_body0));
+      pix = kIdle;
+      FRM_SUB_END(3);
     }
     // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
 #ifdef FRM_STAMPS
@@ -301,9 +285,13 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     // 3. start the next DE of every lane that needs one (the hit point of the normal
     //    taps is recomputed from the unchanged primary ray: ray_at(o, t_hit, d))
     if (need_point) {
-      need_point = false;
       const v3 r = ray_at(o, t, d);
-      q = (phase - kTap0 <= kTap3 - kTap0) ? normal_tap_pos(r, (int)(phase - kTap0)) : r;
+      // normal tap k samples r + s_k * MIN_DISTANCE (normal_tap_pos), with selects
+      const uint32_t kq = phase - kTap0;
+      const bool is_tap = kq <= kTap3 - kTap0;
+      const float e = kMinDistance;
+      const float ex = (kq == 0u || kq == 3u) ? e : -e, ey = (kq >= 2u) ? e : -e, ez = (kq == 1u || kq == 3u) ? e : -e;
+      q = mk(is_tap ? r.x + ex : r.x, is_tap ? r.y + ey : r.y, is_tap ? r.z + ez : r.z);
       if constexpr (FAM == kMandelbulb) {
         z = q;
         dr = 1.f;

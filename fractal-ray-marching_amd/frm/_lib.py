@@ -124,6 +124,15 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise OSError(f"{LIB_PATH} not found: build it with `make -C {PKG_ROOT}` "
                       "(there is no CPU fallback)")
+    # One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64 with the same
+    # SONAME (libamdhip64.so.7) as /opt/rocm's: when torch is loaded first, libfrm binds to
+    # that copy, so torch streams, events and torch.cuda.synchronize() and libfrm share one
+    # runtime. Loaded the other way round, torch would bring up a second runtime and fail
+    # ("No HIP GPUs are available"). Plain C users of libfrm get /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, restype, argtypes in SIGNATURES:
         fn = getattr(lib, name)
