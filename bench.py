@@ -150,7 +150,20 @@ def main():
 
     tf = RowTiledFrame(w.width, w.height, rank, world, band_rows, dev, render_bands, unshuffle)
 
-    tf.run(args.warmup)
+    # Animated workloads (C5): every frame advances time by 1/60 s through the reference's
+    # Timing::update (frm_timing_update), as the reference's frame loop does
+    # (initialized_app.rs:43-48); frame k of the run renders at time + k/60.
+    clock = frm.Timing()
+    frames_issued = [0]
+    before_frame = None
+    if w.animated:
+        def before_frame(k):
+            if frames_issued[0] > 0:
+                clock.update(params, 1.0 / 60.0)
+                r.update_parameters_buffer(params)
+            frames_issued[0] += 1
+
+    tf.run(args.warmup, before_frame)
     torch.cuda.synchronize()
     counters.zero_()
     if world > 1:
@@ -158,7 +171,7 @@ def main():
     torch.cuda.synchronize()
     timing["on"] = True
     t0 = time.perf_counter()
-    tf.run(args.steps)
+    tf.run(args.steps, before_frame)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -197,6 +210,7 @@ def main():
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
                 "pose": args.pose, "kernel": args.kernel,
+                "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
                 "parallelism": f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if world > 1
                                else "single GPU",
             },

@@ -203,3 +203,135 @@ extern "C" void frm_parameters_update_camera(frm_parameters* p, const float posi
   for (int r = 0; r < 4; ++r)
     for (int k = 0; k < 4; ++k) p->camera_matrix[4 * r + k] = c[r][k];
 }
+
+// ---- animation driver: src/camera.rs + src/timing.rs -----------------
+// Plain f32 arithmetic in cgmath's operation order (no contraction: -ffp-contract=off),
+// f32 libm for sin/cos/atan2/exp like Rust's f32 methods.
+namespace {
+
+constexpr float kFullTurn = 6.2831855f;        // Rad::<f32>::full_turn() = f32(2 pi)
+constexpr float kMaxPitch = 1.5707964f;        // FRAC_PI_2, camera.rs:156
+constexpr float kRotationPerSecond = 0.5f;     // camera.rs:46
+constexpr float kRotationPerPixel = 0.0003f;   // camera.rs:149
+
+// utils.rs:62-69
+float limited_quadratic_delta(float current, float delta) {
+  float factor = current == 0.0f ? 0.025f : fminf(fmaxf(fabsf(current), 0.0001f), 0.1f);
+  return 0.2f * delta * factor;
+}
+
+// held_keys.rs:32-34: i8 difference of two held flags
+float magnitude(uint32_t keys, uint32_t positive, uint32_t negative) {
+  return (float)((int)((keys & positive) != 0) - (int)((keys & negative) != 0));
+}
+
+void add_pitch(frm_camera* c, float pitch) {  // camera.rs:159-169 (num_traits::clamp)
+  float v = c->pitch + pitch;
+  c->pitch = v < -kMaxPitch ? -kMaxPitch : (v > kMaxPitch ? kMaxPitch : v);
+}
+
+void add_yaw(frm_camera* c, float yaw) {  // camera.rs:163-173: Rad % Rad is f32 fmod
+  c->yaw = fmodf(c->yaw + yaw, kFullTurn);
+}
+
+}  // namespace
+
+extern "C" void frm_camera_default(frm_camera* c) {
+  if (!c) return;
+  memset(c, 0, sizeof(*c));
+  c->movement_per_second = 1.0f;
+  c->position[2] = -1.0f;
+  c->lock_yaw_mode = FRM_LOCK_YAW_NONE;
+}
+
+extern "C" void frm_camera_update(frm_camera* c, uint32_t keys, float seconds) {
+  if (!c) return;
+  // do_movement (camera.rs:107-117): forward = yaw_matrix().z, right = yaw_matrix().x
+  const float sy = sinf(c->yaw), cy = cosf(c->yaw);
+  const float fm = magnitude(keys, FRM_KEY_MOVE_FORWARD, FRM_KEY_MOVE_BACKWARD);
+  const float rm = magnitude(keys, FRM_KEY_MOVE_RIGHT, FRM_KEY_MOVE_LEFT);
+  const float um = magnitude(keys, FRM_KEY_MOVE_UP, FRM_KEY_MOVE_DOWN);
+  const float mv[3] = {(sy * fm + cy * rm) + 0.0f * um, (0.0f * fm + 0.0f * rm) + 1.0f * um,
+                       (cy * fm + -sy * rm) + 0.0f * um};
+  if (!(mv[0] == 0.0f && mv[1] == 0.0f && mv[2] == 0.0f)) {
+    // normalize_to(m) = v * (m / |v|), |v| = sqrt((x*x + y*y) + z*z)
+    const float len = sqrtf((mv[0] * mv[0] + mv[1] * mv[1]) + mv[2] * mv[2]);
+    const float s = (c->movement_per_second * seconds) / len;
+    for (int k = 0; k < 3; ++k) c->position[k] = c->position[k] + mv[k] * s;
+  }
+  const float rot = kRotationPerSecond * seconds;
+  add_pitch(c, rot * magnitude(keys, FRM_KEY_PITCH_DOWN, FRM_KEY_PITCH_UP));
+  add_yaw(c, rot * magnitude(keys, FRM_KEY_YAW_RIGHT, FRM_KEY_YAW_LEFT));
+  // do_orbit (camera.rs:119-122): Matrix3::from_angle_y(a) * p, rows (c,0,s),(0,1,0),(-s,0,c)
+  const float a = c->orbit_angle_per_second * seconds;
+  const float so = sinf(a), co = cosf(a);
+  const float p0 = c->position[0], p1 = c->position[1], p2 = c->position[2];
+  c->position[0] = (co * p0 + 0.0f * p1) + so * p2;
+  c->position[1] = (0.0f * p0 + 1.0f * p1) + 0.0f * p2;
+  c->position[2] = (-so * p0 + 0.0f * p1) + co * p2;
+  // do_lock_rotation (camera.rs:124-147)
+  if (c->lock_yaw_mode != FRM_LOCK_YAW_NONE) {
+    float offset = 0.0f;
+    switch (c->lock_yaw_mode) {
+      case FRM_LOCK_YAW_INWARDS: offset = -kFullTurn / 2.0f; break;
+      case FRM_LOCK_YAW_RIGHT: offset = -kFullTurn / 4.0f; break;
+      case FRM_LOCK_YAW_LEFT: offset = kFullTurn / 4.0f; break;
+      default: offset = 0.0f; break;  // Outwards
+    }
+    c->yaw = atan2f(c->position[0], c->position[2]) + offset;
+  }
+  if (c->lock_pitch) {
+    const float radius = sqrtf(c->position[0] * c->position[0] + c->position[2] * c->position[2]);
+    c->pitch = atan2f(c->position[1], radius);
+  }
+}
+
+extern "C" void frm_camera_update_speed(frm_camera* c, float delta) {
+  if (c) c->movement_per_second = c->movement_per_second * expf(delta * 0.1f);
+}
+
+extern "C" void frm_camera_update_orbit_speed(frm_camera* c, float delta) {
+  if (c) c->orbit_angle_per_second = c->orbit_angle_per_second + limited_quadratic_delta(c->orbit_angle_per_second, delta);
+}
+
+extern "C" void frm_camera_reset_orbit_speed(frm_camera* c) {
+  if (c) c->orbit_angle_per_second = 0.0f;
+}
+
+extern "C" void frm_camera_toggle_lock_pitch(frm_camera* c) {
+  if (c) c->lock_pitch = !c->lock_pitch;
+}
+
+extern "C" void frm_camera_cycle_lock_yaw_mode(frm_camera* c, int32_t backwards) {
+  if (!c) return;
+  // None -> Inwards -> Right -> Outwards -> Left -> None (backwards: the reverse)
+  const int32_t m = c->lock_yaw_mode < 0 || c->lock_yaw_mode > 4 ? 0 : c->lock_yaw_mode;
+  c->lock_yaw_mode = backwards ? (m + 4) % 5 : (m + 1) % 5;
+}
+
+extern "C" void frm_camera_rotate_from_cursor(frm_camera* c, float yaw_pixels, float pitch_pixels) {
+  if (!c) return;
+  add_pitch(c, kRotationPerPixel * pitch_pixels);
+  add_yaw(c, kRotationPerPixel * yaw_pixels);
+}
+
+extern "C" void frm_parameters_update_camera_from(frm_parameters* p, const frm_camera* c) {
+  if (p && c) frm_parameters_update_camera(p, c->position, c->yaw, c->pitch);
+}
+
+extern "C" void frm_timing_init(frm_timing* t) {
+  if (t) t->time_factor = 1.0f;
+}
+
+extern "C" float frm_timing_update(frm_timing* t, frm_parameters* p, float delta_seconds) {
+  if (t && p) frm_parameters_update_time(p, t->time_factor * delta_seconds);
+  return delta_seconds;
+}
+
+extern "C" void frm_timing_update_time_factor(frm_timing* t, float delta) {
+  if (t) t->time_factor = t->time_factor + limited_quadratic_delta(t->time_factor, delta);
+}
+
+extern "C" void frm_timing_stop_time(frm_timing* t) {
+  if (t) t->time_factor = 0.0f;
+}

@@ -6,12 +6,12 @@ src/graphics.rs) over the C ABI of include/frm.h (libfrm.so, HIP kernels for gfx
 from ._lib import (FRM_DEFAULT_MAX_STEPS, FRM_FLAG_SCENE_SPHERE, FRM_FLAG_SIMPLE_KERNEL,
                    FRM_MAX_NUM_ITERATIONS, FRM_NUM_COUNTERS, FRM_NUM_SCENES, FrmError, LIB_PATH,
                    load)
-from .parameters import Camera, Parameters
+from .parameters import Camera, HeldKeys, Parameters, Timing
 from .renderer import Renderer, device_count
 from .workloads import POSES, POWER8_TIME, WORKLOADS, Workload, make_parameters
 
 __all__ = [
-    "Camera", "Parameters", "Renderer", "FrmError", "device_count", "load", "LIB_PATH",
+    "Camera", "HeldKeys", "Parameters", "Renderer", "Timing", "FrmError", "device_count", "load", "LIB_PATH",
     "POSES", "POWER8_TIME", "WORKLOADS", "Workload", "make_parameters",
     "FRM_DEFAULT_MAX_STEPS", "FRM_FLAG_SCENE_SPHERE", "FRM_FLAG_SIMPLE_KERNEL",
     "FRM_MAX_NUM_ITERATIONS", "FRM_NUM_COUNTERS", "FRM_NUM_SCENES",

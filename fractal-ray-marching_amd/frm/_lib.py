@@ -68,6 +68,24 @@ class FrmStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class FrmCamera(ctypes.Structure):
+    """frm_camera (include/frm.h): src/camera.rs:5-14."""
+
+    _fields_ = [
+        ("position", ctypes.c_float * 3),
+        ("pitch", ctypes.c_float),
+        ("yaw", ctypes.c_float),
+        ("movement_per_second", ctypes.c_float),
+        ("orbit_angle_per_second", ctypes.c_float),
+        ("lock_yaw_mode", ctypes.c_int32),
+        ("lock_pitch", ctypes.c_int32),
+    ]
+
+
+class FrmTiming(ctypes.Structure):
+    _fields_ = [("time_factor", ctypes.c_float)]
+
+
 assert ctypes.sizeof(FrmParameters) == 96
 
 _P = ctypes.POINTER
@@ -105,6 +123,19 @@ SIGNATURES = [
     ("frm_parameters_update_scene_index", None, [_P(FrmParameters), ctypes.c_int32]),
     ("frm_parameters_update_camera", None,
      [_P(FrmParameters), _P(ctypes.c_float), ctypes.c_float, ctypes.c_float]),
+    ("frm_camera_default", None, [_P(FrmCamera)]),
+    ("frm_camera_update", None, [_P(FrmCamera), ctypes.c_uint32, ctypes.c_float]),
+    ("frm_camera_update_speed", None, [_P(FrmCamera), ctypes.c_float]),
+    ("frm_camera_update_orbit_speed", None, [_P(FrmCamera), ctypes.c_float]),
+    ("frm_camera_reset_orbit_speed", None, [_P(FrmCamera)]),
+    ("frm_camera_toggle_lock_pitch", None, [_P(FrmCamera)]),
+    ("frm_camera_cycle_lock_yaw_mode", None, [_P(FrmCamera), ctypes.c_int32]),
+    ("frm_camera_rotate_from_cursor", None, [_P(FrmCamera), ctypes.c_float, ctypes.c_float]),
+    ("frm_parameters_update_camera_from", None, [_P(FrmParameters), _P(FrmCamera)]),
+    ("frm_timing_init", None, [_P(FrmTiming)]),
+    ("frm_timing_update", ctypes.c_float, [_P(FrmTiming), _P(FrmParameters), ctypes.c_float]),
+    ("frm_timing_update_time_factor", None, [_P(FrmTiming), ctypes.c_float]),
+    ("frm_timing_stop_time", None, [_P(FrmTiming)]),
 ]
 
 _lib = None

@@ -54,11 +54,14 @@ class RowTiledFrame:
                 self.unshuffle(self.gathered[k % 2], self.frame)
         self.frames_done += 1
 
-    def run(self, n):
+    def run(self, n, before_frame=None):
         """Render, gather and reassemble n frames (asynchronous on the GPU path: callers
-        synchronize the device to wait for the last one)."""
+        synchronize the device to wait for the last one). before_frame(k), if given, runs on
+        the host before frame k is issued (e.g. to advance animated parameters)."""
         pending = None
         for k in range(n):
+            if before_frame is not None:
+                before_frame(k)
             work = self._issue(k)
             if pending is not None:
                 self._finish(*pending)

@@ -27,6 +27,7 @@ class Workload:
     time: float
     sphere: bool = False
     note: str = ""
+    animated: bool = False  # frame k renders at time + k/60
 
 
 WORKLOADS = {
@@ -39,7 +40,7 @@ WORKLOADS = {
     "C4": Workload("C4-mandelbulb-8k", 7680, 4320, 18, 16, 512, POWER8_TIME,
                    note="7680x4320 Mandelbulb, 16 iters, 512 steps"),
     "C5": Workload("C5-mandelbulb-16k", 16384, 16384, 18, 20, 1024, POWER8_TIME,
-                   note="16384x16384 animated Mandelbulb, 20 iters, 1024 steps"),
+                   note="16384x16384 animated Mandelbulb, 20 iters, 1024 steps", animated=True),
     "HEADLINE": Workload("headline-mandelbulb-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
                          note="3840x2160 Mandelbulb power 8, 12 iters, 256 steps"),
 }

@@ -190,6 +190,61 @@ void frm_parameters_update_scene_index(frm_parameters* p, int32_t delta);    /* 
 void frm_parameters_update_camera(frm_parameters* p, const float position[3], float yaw,
                                   float pitch);
 
+/* ---- animation driver: host-side restatement of the reference's Camera (src/camera.rs)
+ *      and Timing (src/timing.rs), for scripted fly-throughs without a window (SURVEY
+ *      §8(f) row 2). Keyboard/mouse input becomes explicit arguments: held keys as a
+ *      FRM_KEY_* bit set (held_keys.rs), the frame time as seconds (timing.rs uses
+ *      Instant::now). All arithmetic is f32 in cgmath's operation order. */
+#define FRM_KEY_MOVE_FORWARD (1u << 0)  /* held_keys.rs:6-17 */
+#define FRM_KEY_MOVE_BACKWARD (1u << 1)
+#define FRM_KEY_MOVE_RIGHT (1u << 2)
+#define FRM_KEY_MOVE_LEFT (1u << 3)
+#define FRM_KEY_MOVE_UP (1u << 4)
+#define FRM_KEY_MOVE_DOWN (1u << 5)
+#define FRM_KEY_PITCH_UP (1u << 6)
+#define FRM_KEY_PITCH_DOWN (1u << 7)
+#define FRM_KEY_YAW_RIGHT (1u << 8)
+#define FRM_KEY_YAW_LEFT (1u << 9)
+
+enum { /* camera.rs:16-23 */
+  FRM_LOCK_YAW_NONE = 0,
+  FRM_LOCK_YAW_INWARDS = 1,
+  FRM_LOCK_YAW_RIGHT = 2,
+  FRM_LOCK_YAW_OUTWARDS = 3,
+  FRM_LOCK_YAW_LEFT = 4
+};
+
+typedef struct frm_camera { /* camera.rs:5-14 */
+  float position[3];
+  float pitch;                  /* radians, clamped to [-pi/2, pi/2]          */
+  float yaw;                    /* radians, kept in (-2pi, 2pi) by fmod        */
+  float movement_per_second;
+  float orbit_angle_per_second; /* radians per second about the y axis         */
+  int32_t lock_yaw_mode;        /* FRM_LOCK_YAW_*                              */
+  int32_t lock_pitch;           /* bool                                        */
+} frm_camera;
+
+void frm_camera_default(frm_camera* c);                                  /* camera.rs:176-188 */
+void frm_camera_update(frm_camera* c, uint32_t held_keys, float seconds); /* camera.rs:100-147 */
+void frm_camera_update_speed(frm_camera* c, float delta);                /* camera.rs:60-62 */
+void frm_camera_update_orbit_speed(frm_camera* c, float delta);          /* camera.rs:64-69 */
+void frm_camera_reset_orbit_speed(frm_camera* c);                        /* camera.rs:71-73 */
+void frm_camera_toggle_lock_pitch(frm_camera* c);                        /* camera.rs:75-77 */
+void frm_camera_cycle_lock_yaw_mode(frm_camera* c, int32_t backwards);   /* camera.rs:79-98 */
+void frm_camera_rotate_from_cursor(frm_camera* c, float yaw_pixels,
+                                   float pitch_pixels);                  /* camera.rs:151-154 */
+void frm_parameters_update_camera_from(frm_parameters* p, const frm_camera* c); /* parameters.rs:23-25 */
+
+typedef struct frm_timing { /* timing.rs:5-10, minus the wall clock and the FPS log */
+  float time_factor;
+} frm_timing;
+
+void frm_timing_init(frm_timing* t);                                     /* timing.rs:13-21 */
+/* parameters.time += time_factor * delta_seconds (timing.rs:23-30); returns delta_seconds */
+float frm_timing_update(frm_timing* t, frm_parameters* p, float delta_seconds);
+void frm_timing_update_time_factor(frm_timing* t, float delta);          /* timing.rs:32-34 */
+void frm_timing_stop_time(frm_timing* t);                                /* timing.rs:36-38 */
+
 #ifdef __cplusplus
 }
 #endif

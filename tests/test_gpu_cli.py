@@ -1,0 +1,61 @@
+"""§8(f) rows 1-2 on the GPU: the offscreen CLI (bin/frm_render) renders a scripted
+fly-through — held keys, orbit, yaw/pitch locks and time advancing per frame through
+libfrm's Camera/Timing restatement — and every PPM it writes equals the oracle's render of
+the same frame, whose parameters are replayed here through the Python mirror."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import frm
+
+pytestmark = pytest.mark.gpu
+
+EXE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fractal-ray-marching_amd",
+                   "bin", "frm_render")
+
+
+def read_ppm(path):
+    with open(path, "rb") as fh:
+        data = fh.read()
+    header, rest = data.split(b"\n", 1)
+    dims, rest = rest.split(b"\n", 1)
+    maxv, pix = rest.split(b"\n", 1)
+    w, h = (int(v) for v in dims.split())
+    assert header == b"P6" and maxv == b"255"
+    return np.frombuffer(pix, np.uint8).reshape(h, w, 3)
+
+
+def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib):
+    W, H, frames, dt, keys, orbit = 96, 54, 3, 0.05, frm.HeldKeys.MOVE_FORWARD | frm.HeldKeys.YAW_LEFT, 2.0
+    pos, iters, time, steps = (1.5, 0.9, -1.5), 6, frm.POWER8_TIME, 256
+    out = str(tmp_path / "f_%02d.ppm")
+    cmd = [EXE, "--width", str(W), "--height", str(H), "--frames", str(frames), "--dt", str(dt),
+           "--keys", str(keys), "--orbit", str(orbit), "--lock-pitch", "--pos", *map(str, pos),
+           "--iters", str(iters), "--time", str(time), "--max-steps", str(steps), "--scene", "18", "--out", out]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    lines = [json.loads(l) for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == frames
+
+    # replay: initialized_app.rs:43-48 with the same frame time
+    p = frm.Parameters()
+    p.update_aspect(W, H)
+    p.time, p.num_iterations, p.scene_index = time, iters, 18
+    cam = frm.Camera(pos, 0.0, 0.0)
+    cam.raw.orbit_angle_per_second = orbit
+    cam.raw.lock_pitch = 1
+    timing = frm.Timing()
+    p.update_camera(cam)
+    for fr in range(frames):
+        if fr > 0:
+            delta = timing.update(p, dt)
+            cam.update(keys, delta)
+            p.update_camera(cam)
+        assert lines[fr]["pos"] == pytest.approx(list(cam.position), abs=1e-5)
+        ref = oracle.render(p, W, H, steps)
+        got = read_ppm(out % fr)
+        assert np.array_equal(got, ref["rgba"][..., :3]), f"frame {fr}"
+        assert lines[fr]["march_steps"] == int(ref["counters"][2]) + int(ref["counters"][3])

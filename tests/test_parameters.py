@@ -79,8 +79,8 @@ def test_default_camera_pose():
 
 def test_forward_vector_convention():
     cam = frm.Camera((0, 0, 0), math.pi / 2, 0)  # yaw_matrix().z = (sin yaw, 0, cos yaw)
-    f = cam.forward()
-    assert abs(f[0] - 1) < 1e-12 and abs(f[2]) < 1e-12
+    f = cam.forward()  # yaw is an f32 (camera.rs:13): cos(f32(pi/2)) = -4.37e-8
+    assert abs(f[0] - 1) < 1e-12 and abs(f[2]) < 1e-7
 
 
 def test_parameters_blob_roundtrip():
