@@ -31,6 +31,8 @@ struct frm_ctx {
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   uint32_t width = 0, height = 0;
   uint8_t* fb = nullptr;
+  uint8_t* present_buf = nullptr;  // frm_present output, grown on demand
+  size_t present_cap = 0;
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   unsigned int* queue = nullptr;
   ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
@@ -244,6 +246,7 @@ int frm_destroy(frm_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->fb) (void)hipFree(ctx->fb);
+  if (ctx->present_buf) (void)hipFree(ctx->present_buf);
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->queue) (void)hipFree(ctx->queue);
   if (ctx->records) (void)hipFree(ctx->records);
@@ -320,6 +323,32 @@ int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes) {
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, frame needs %zu", dst_bytes, need);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->fb, need, hipMemcpyDeviceToHost, ctx->stream));
+  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return FRM_OK;
+}
+
+int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags, uint8_t* dst,
+                size_t dst_bytes) {
+  if (!ctx || !dst) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/dst is NULL");
+  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (out_width == 0 || out_height == 0 || out_width > FRM_MAX_DIMENSION || out_height > FRM_MAX_DIMENSION)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad output size %ux%u", out_width, out_height);
+  if (flags & ~(FRM_BLIT_SRGB | FRM_BLIT_BGRA)) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
+  const size_t need = (size_t)out_width * out_height * 4u;
+  if (dst_bytes < need)
+    return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, output needs %zu", dst_bytes, need);
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (need > ctx->present_cap) {
+    FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->present_buf) FRM_HIP(ctx, hipFree(ctx->present_buf));
+    ctx->present_buf = nullptr;
+    ctx->present_cap = 0;
+    FRM_HIP(ctx, hipMalloc(&ctx->present_buf, need));
+    ctx->present_cap = need;
+  }
+  FRM_HIP(ctx, launch_blit(ctx->fb, ctx->width, ctx->height, ctx->present_buf, out_width, out_height, flags,
+                           ctx->stream));
+  FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->present_buf, need, hipMemcpyDeviceToHost, ctx->stream));
   FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return FRM_OK;
 }

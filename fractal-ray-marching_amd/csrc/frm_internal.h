@@ -39,6 +39,8 @@ struct KernelArgs {
 // frm_kernels.hip
 enum KernelKind : uint32_t { kKernelPersistent = 0, kKernelSimple = 1 };
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream);
+hipError_t launch_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
+                       uint32_t flags, hipStream_t stream);
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,
                             uint32_t height, uint32_t band_rows, uint32_t ranks,
                             hipStream_t stream);

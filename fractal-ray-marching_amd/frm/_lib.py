@@ -26,6 +26,8 @@ FRM_MAX_NUM_ITERATIONS = 4096
 FRM_NUM_COUNTERS = 8
 FRM_FLAG_SCENE_SPHERE = 0x1
 FRM_FLAG_SIMPLE_KERNEL = 0x2
+FRM_BLIT_SRGB = 0x1
+FRM_BLIT_BGRA = 0x2
 
 
 class FrmParameters(ctypes.Structure):
@@ -103,6 +105,8 @@ SIGNATURES = [
     ("frm_render", ctypes.c_int, [ctypes.c_void_p, _P(FrmStats)]),
     ("frm_read_frame", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_synchronize", ctypes.c_int, [ctypes.c_void_p]),
+    ("frm_present", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_band_rows_for", ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint32)]),
     ("frm_render_bands", ctypes.c_int,

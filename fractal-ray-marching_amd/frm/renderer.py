@@ -63,6 +63,13 @@ class Renderer:
         self._check(self._lib.frm_read_frame(self.ctx, buf.ctypes.data, buf.nbytes))
         return buf
 
+    # blit.wgsl + present (graphics.rs:91-110): the frame resampled to a window size
+    def present(self, width, height, srgb=True, bgra=False):
+        buf = np.empty((height, width, 4), dtype=np.uint8)
+        flags = (_lib.FRM_BLIT_SRGB if srgb else 0) | (_lib.FRM_BLIT_BGRA if bgra else 0)
+        self._check(self._lib.frm_present(self.ctx, width, height, flags, buf.ctypes.data, buf.nbytes))
+        return buf
+
     def synchronize(self):
         self._check(self._lib.frm_synchronize(self.ctx))
 

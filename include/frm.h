@@ -133,6 +133,19 @@ int frm_render(frm_ctx* ctx, frm_stats* stats);
 /* ---- readback (replaces the blit pass + present, graphics.rs:101-108). Copies the
  *      whole RGBA8 sRGB frame (row 0 = top, 4*width*height bytes) to host memory. */
 int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes);
+
+/* Present the last rendered frame at out_width x out_height into host dst (RGBA8 or BGRA8,
+ * pitch 4*out_width): the reference's blit pass, which draws the render texture on the
+ * window surface (blit.wgsl:6-11; graphics.rs:91-110) through a clamp-to-edge sampler with
+ * linear magnification and nearest minification (persistent_graphics.rs:55-64), texels
+ * read as linear light (the texture is Rgba8UnormSrgb, blit_graphics.rs:14). The surface
+ * format is platform-chosen (persistent_graphics.rs:95): FRM_BLIT_SRGB encodes the output
+ * as sRGB (an ...UnormSrgb surface) instead of linear unorm, FRM_BLIT_BGRA writes B,G,R,A.
+ * Synchronous. Same size + FRM_BLIT_SRGB reproduces frm_read_frame's bytes. */
+#define FRM_BLIT_SRGB 0x1u
+#define FRM_BLIT_BGRA 0x2u
+int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags, uint8_t* dst,
+                size_t dst_bytes);
 int frm_synchronize(frm_ctx* ctx);
 
 /* ---- row-tiled rendering for multi-GPU (no reference counterpart: the reference

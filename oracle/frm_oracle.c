@@ -709,3 +709,69 @@ int om_frame_info(const uint8_t* params96, uint32_t flags, int mode, float* out8
   out8[7] = F.origin.z;
   return 0;
 }
+
+/* ---- presentation resample: blit.wgsl:6-11 through the sampler of
+ * persistent_graphics.rs:55-64 (clamp to edge, linear magnification, nearest
+ * minification), texels of the Rgba8UnormSrgb render texture (blit_graphics.rs:14) read as
+ * linear light. Restated independently of the kernel: the decode table is the closed-form
+ * inverse transfer function in long double, rounded once to f32. flags: 1 = encode the
+ * output as sRGB (an ...Srgb surface), else linear unorm; 2 = B,G,R,A byte order. */
+static float g_srgb_dec[256];
+static pthread_once_t g_dec_once = PTHREAD_ONCE_INIT;
+static void dec_init(void) {
+  for (int k = 0; k < 256; ++k) {
+    long double s = (long double)k / 255.0L;
+    long double lin = s <= 0.04045L ? s / 12.92L : powl((s + 0.055L) / 1.055L, 2.4L);
+    g_srgb_dec[k] = (float)lin;
+  }
+}
+static float mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+static uint8_t out_channel(float c, uint32_t flags) {
+  if (flags & 1u) return encode(c);
+  return (uint8_t)rintf(fminf(fmaxf(c, 0.0f), 1.0f) * 255.0f);
+}
+static uint32_t clampi(int v, uint32_t n) { return v < 0 ? 0u : ((uint32_t)v >= n ? n - 1u : (uint32_t)v); }
+
+void om_srgb_decode(float* out256) {
+  pthread_once(&g_dec_once, dec_init);
+  memcpy(out256, g_srgb_dec, sizeof(g_srgb_dec));
+}
+
+int om_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
+            uint32_t flags) {
+  if (!src || !dst || !sw || !sh || !dw || !dh) return 1;
+  pthread_once(&g_srgb_once, srgb_init);
+  pthread_once(&g_dec_once, dec_init);
+  const int magnify = (float)sw / (float)dw <= 1.0f && (float)sh / (float)dh <= 1.0f;
+  for (uint32_t y = 0; y < dh; ++y)
+    for (uint32_t x = 0; x < dw; ++x) {
+      /* vertex.wgsl's varyings at the pixel centre, then blit.wgsl:8-9 */
+      const float sx = (float)(2u * x + 1u) / (float)dw - 1.0f;
+      const float sy = 1.0f - (float)(2u * y + 1u) / (float)dh;
+      const float u = (sx + 1.0f) * 0.5f, v = 1.0f - (sy + 1.0f) * 0.5f;
+      float ch[3];
+      if (magnify) {
+        const float tu = u * (float)sw - 0.5f, tv = v * (float)sh - 0.5f;
+        const float fu = floorf(tu), fv = floorf(tv), a = tu - fu, c = tv - fv;
+        const uint32_t x0 = clampi((int)fu, sw), x1 = clampi((int)fu + 1, sw);
+        const uint32_t y0 = clampi((int)fv, sh), y1 = clampi((int)fv + 1, sh);
+        for (int k = 0; k < 3; ++k) {
+          const float t00 = g_srgb_dec[src[4 * ((size_t)y0 * sw + x0) + k]];
+          const float t10 = g_srgb_dec[src[4 * ((size_t)y0 * sw + x1) + k]];
+          const float t01 = g_srgb_dec[src[4 * ((size_t)y1 * sw + x0) + k]];
+          const float t11 = g_srgb_dec[src[4 * ((size_t)y1 * sw + x1) + k]];
+          ch[k] = mixf(mixf(t00, t10, a), mixf(t01, t11, a), c);
+        }
+      } else {
+        const uint32_t ix = clampi((int)floorf(u * (float)sw), sw), iy = clampi((int)floorf(v * (float)sh), sh);
+        for (int k = 0; k < 3; ++k) ch[k] = g_srgb_dec[src[4 * ((size_t)iy * sw + ix) + k]];
+      }
+      uint8_t* o = dst + 4 * ((size_t)y * dw + x);
+      const uint8_t r = out_channel(ch[0], flags), g = out_channel(ch[1], flags), b = out_channel(ch[2], flags);
+      o[0] = (flags & 2u) ? b : r;
+      o[1] = g;
+      o[2] = (flags & 2u) ? r : b;
+      o[3] = 255;
+    }
+  return 0;
+}

@@ -51,6 +51,11 @@ def load():
         lib.om_srgb_thresholds.restype = None
         lib.om_encode_srgb.argtypes = [f32p, ctypes.c_uint32, u8p]
         lib.om_encode_srgb.restype = ctypes.c_int
+        lib.om_srgb_decode.argtypes = [f32p]
+        lib.om_srgb_decode.restype = None
+        lib.om_blit.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                ctypes.c_uint32]
+        lib.om_blit.restype = ctypes.c_int
         lib.om_frame_info.argtypes = [u8p, ctypes.c_uint32, ctypes.c_int, f32p]
         lib.om_frame_info.restype = ctypes.c_int
         _lib = lib
@@ -134,3 +139,21 @@ def frame_info(params, flags=0, mode=MODE_FRM):
     return {"family": int(out[0]), "mb_power": float(out[1]), "menger_cross": float(out[2]),
             "menger_scale": float(out[3]), "koch_normal_z": float(out[4]),
             "origin": tuple(float(v) for v in out[5:8])}
+
+
+def srgb_decode():
+    out = np.zeros(256, dtype=np.float32)
+    load().om_srgb_decode(out.ctypes.data)
+    return out
+
+
+def blit(rgba, out_width, out_height, flags=1):
+    """Presentation resample of an RGBA8 sRGB frame [H, W, 4] (om_blit): flags 1 = sRGB output,
+    2 = BGRA byte order."""
+    src = np.ascontiguousarray(rgba, dtype=np.uint8)
+    h, w = src.shape[:2]
+    out = np.zeros((out_height, out_width, 4), dtype=np.uint8)
+    rc = load().om_blit(src.ctypes.data, w, h, out.ctypes.data, out_width, out_height, flags)
+    if rc != 0:
+        raise ValueError("om_blit")
+    return out
