@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
+                    "copy of csrc/ (frm_reload, hiprtc)")
     return ap.parse_args()
 
 
@@ -123,6 +125,8 @@ def main():
     r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags)
     r.resize(w.width, w.height)
     r.update_parameters_buffer(params)
+    if args.reload:
+        r.reload(args.reload)
 
     band_rows = args.band_rows or (w.height if world == 1 else tiling.choose_band_rows(w.height, world))
     dev = torch.device("cuda", local)
@@ -209,7 +213,7 @@ def main():
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
-                "pose": args.pose, "kernel": args.kernel,
+                "pose": args.pose, "kernel": args.kernel + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
                 "parallelism": f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if world > 1
                                else "single GPU",

@@ -31,6 +31,7 @@ struct frm_ctx {
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   uint32_t width = 0, height = 0;
   uint8_t* fb = nullptr;
+  ReloadedKernels* reloaded = nullptr;  // frm_reload: kernels compiled from edited sources
   uint8_t* present_buf = nullptr;  // frm_present output, grown on demand
   size_t present_cap = 0;
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
@@ -58,7 +59,7 @@ namespace {
 thread_local std::string g_error;  // failures without a context
 
 int fail(frm_ctx* ctx, int code, const char* fmt, ...) {
-  char buf[512];
+  char buf[8192];  // room for a compiler log (frm_reload)
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
@@ -176,7 +177,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
     FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 16, 0, 8, s));
 #endif
   }
-  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s));
+  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded));
   return FRM_OK;
 }
 
@@ -247,6 +248,7 @@ int frm_destroy(frm_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->fb) (void)hipFree(ctx->fb);
   if (ctx->present_buf) (void)hipFree(ctx->present_buf);
+  unload_reloaded(ctx->reloaded);
   if (ctx->counters) (void)hipFree(ctx->counters);
   if (ctx->queue) (void)hipFree(ctx->queue);
   if (ctx->records) (void)hipFree(ctx->records);
@@ -350,6 +352,22 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
                            ctx->stream));
   FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->present_buf, need, hipMemcpyDeviceToHost, ctx->stream));
   FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return FRM_OK;
+}
+
+int frm_reload(frm_ctx* ctx, const char* source_dir) {
+  if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  ReloadedKernels* rk = nullptr;
+  if (source_dir) {
+    std::string log;
+    const int rc = compile_reloaded(source_dir, ctx->device, &rk, &log);
+    if (rc != FRM_OK) return fail(ctx, rc, "reload failed, previous kernels kept: %s", log.c_str());
+  }
+  // the old module may still run, on this context's stream or a caller's (frm_render_bands)
+  FRM_HIP(ctx, hipDeviceSynchronize());
+  unload_reloaded(ctx->reloaded);
+  ctx->reloaded = rk;
   return FRM_OK;
 }
 

@@ -1,6 +1,10 @@
 // frm_internal.h — declarations shared by libfrm's translation units (not installed).
 #pragma once
+#if !defined(__HIPCC_RTC__)  // hiprtc (frm_reload) provides the HIP runtime itself
 #include <hip/hip_runtime.h>
+
+#include <string>
+#endif
 
 #include "frm_uniforms.h"
 
@@ -36,9 +40,25 @@ struct KernelArgs {
   uint8_t* pixel_key;             // persistent kernel: cost key per local pixel (out)
 };
 
-// frm_kernels.hip
+#if !defined(__HIPCC_RTC__)  // host-side launchers; hiprtc only needs the types above
+// Render kernels compiled at run time from edited sources (frm_reload.hip), per DE family
+// (Family in frm_scene.h) and ITERS.
+constexpr uint32_t kNumFamilies = 5;
+struct ReloadedKernels {
+  hipModule_t module = nullptr;
+  hipFunction_t simple[kNumFamilies][2] = {};
+  hipFunction_t persistent[kNumFamilies][2] = {};
+  hipFunction_t shade[kNumFamilies] = {};
+  int persistent_blocks_per_cu[kNumFamilies][2] = {};
+};
+// frm_reload.hip: FRM_OK and *out, or an FRM_ERR_* code and the compiler log in *log.
+int compile_reloaded(const char* dir, int device, ReloadedKernels** out, std::string* log);
+void unload_reloaded(ReloadedKernels* rk);
+
+// frm_kernels.hip (rk: a reloaded module's kernels, or nullptr for the built-in ones)
 enum KernelKind : uint32_t { kKernelPersistent = 0, kKernelSimple = 1 };
-hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream);
+hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
+                         const ReloadedKernels* rk);
 hipError_t launch_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                        uint32_t flags, hipStream_t stream);
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,
@@ -55,5 +75,7 @@ size_t schedule_temp_bytes(uint32_t npix);
 hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
                              hipStream_t stream);
 hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, float* out, hipStream_t stream);
+
+#endif  // !__HIPCC_RTC__
 
 }  // namespace frm

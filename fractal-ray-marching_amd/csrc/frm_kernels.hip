@@ -1,392 +1,16 @@
-// frm_kernels.hip — gfx950 kernels of the fractal ray-marcher.
+// frm_kernels.hip — gfx950 kernels of the fractal ray-marcher and their launchers.
 //
-// render_persistent<FAM>: see below (the default).
-// render_simple<FAM>: one thread per pixel, one wave64 per 8x8 pixel tile (so the 64
-//   lanes of a wave march spatially coherent rays), 256-thread blocks = 16x16 pixels.
-//   Literal restatement of fragment_main (fragment.wgsl:327-349): primary march, on hit
-//   the four normal taps, the shadow march toward the sun and the shading; sRGB encode
-//   and a packed 32-bit RGBA8 store. Work counters are reduced per wave in registers and
-//   added with one 64-bit atomic per wave and counter.
-// unshuffle_bands: rank-major band buffers -> row-major frame (multi-GPU gather).
+// The render kernels (render_simple, march_persistent, shade_pass) live in
+// frm_render_kernels.h so frm_reload can recompile them at run time; this file adds the
+// multi-GPU unshuffle, the presentation blit, the diagnostics kernels (eval_scene,
+// eval_math) and the host launchers, which take a reloaded module's kernels when one is
+// active (frm_reload.hip).
 #include <hip/hip_runtime.h>
 
-#include "frm_internal.h"
-#include "frm_srgb_table.h"
+#include "frm_render_kernels.h"
 
 namespace frm {
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-__device__ __forceinline__ uint32_t band_row_to_global(const BandGeometry& g, uint32_t lr) {
-  uint32_t b = lr / g.band_rows;
-  return (g.first_band + b * g.band_stride) * g.band_rows + (lr - b * g.band_rows);
-}
-
-template <uint32_t FAM, bool ITERS>
-__global__ __launch_bounds__(256) void render_simple(KernelArgs a) {
-  __shared__ float table[256];
-  table[threadIdx.x] = kSrgbThresholds[threadIdx.x];
-  __syncthreads();
-
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-  const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
-  const uint32_t width = a.f.width;
-
-  uint32_t n_pix = 0;
-  PixelCount pc = {0u, 0u, 0u, 0u, {0u, 0u}};
-  if (x < width && lr < a.g.local_rows) {
-    const uint32_t y = band_row_to_global(a.g, lr);
-    if (y < a.f.height) {
-      n_pix = 1;
-      v3 color = shade_pixel<FAM, ITERS>(a.f, a.s, x, y, pc);
-      a.out[(size_t)lr * width + x] = pack_rgba(color, table);
-    }
-  }
-
-  unsigned long long v[7] = {n_pix, pc.hit, pc.primary, pc.shadow, pc.normal, pc.de.bodies, pc.de.bailouts};
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    unsigned long long s = wave_sum(v[k]);
-    if (lane == 0 && s) atomicAdd(&a.counters[k], s);
-  }
-}
-
-// ---- persistent ray-regeneration kernel + deferred shading pass -------------------
-// march_persistent<FAM>: one lane = one pixel at a time, driven by a per-lane state machine
-// over the phases of fragment_main (primary march -> 4 normal taps -> shadow march).
-// Every loop iteration advances every live lane by exactly one unit of DE work: one
-// Mandelbulb loop body (the DE is resumable: z, dr, magnitude and body index live in
-// registers), or one whole DE for the fixed-trip-count families. A lane whose pixel is
-// done takes the next pixel of its wave's current chunk; a wave fetches chunks of 64
-// pixels from a global queue (one atomic per chunk) in the order frm_sched.hip chose
-// (most expensive pixels first), and computes the chunk's 64 camera rays in one coherent
-// pass into LDS. Instead of shading at low lane occupancy, a finished
-// pixel stores a 32-byte ShadeRecord; shade_pass then shades and sRGB-packs all pixels
-// coherently. Per-pixel arithmetic is the same operation sequence as shade_pixel<>, so
-// the bytes are identical to render_simple and the oracle.
-constexpr uint32_t kIdle = 0xFFFFFFFFu;
-constexpr uint32_t kChunk = 64u;  // pixels per queue fetch (one per lane of the fetching wave)
-
-enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
-
-__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(ballot(c)); }
-
-// Scheduling key of a finished pixel: 16 x log2(cost + 1), 0..255 (~4.4 % steps); cost =
-// Mandelbulb bodies, or DE evaluations for the fixed-trip families. Only orders the next
-// frame's fetches; never touches a pixel's bytes.
-__device__ __forceinline__ uint8_t cost_key(uint32_t bodies) {
-  return (uint8_t)min(255.0f, 16.0f * __log2f((float)bodies + 1.0f));
-}
-
-#ifdef FRM_STAMPS
-// diagnostic build: one 16 x u64 record per wave of the last persistent launch
-constexpr uint32_t kWaveDebugSlots = 16384u;
-__device__ unsigned long long g_wave_debug[16u * kWaveDebugSlots];
-#endif
-
-template <uint32_t FAM, bool ITERS>
-#ifndef FRM_MARCH_WAVES_PER_SIMD
-#define FRM_MARCH_WAVES_PER_SIMD 1
-#endif
-__global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
-  __shared__ float4 chunk_rays[4][kChunk];  // per wave: camera ray xyz + local pixel index bits
-
-  const FrameUniforms& f = a.f;
-  const SceneUniforms& su = a.s;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint64_t lane_bit = 1ull << lane;
-  const uint32_t total = a.npix;
-  const uint32_t n_iter = iterations<ITERS>(su.n);
-  ShadeRecord* __restrict__ rec = a.records;
-
-  // wave-uniform state: current chunk of 64 fetched pixels, how many were handed out
-  uint32_t slots_used = kChunk;
-  bool exhausted = false;
-  uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
-
-  // per-lane state
-  uint32_t pix = kIdle;      // local pixel index (lr * width + x) being marched
-  uint32_t phase = kPrimary;
-  bool done = false;         // the current DE has its result
-  v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
-  float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
-  uint32_t it = 0, psteps = 0, body = 0;
-  uint32_t acc_body = 0;   // per-lane Mandelbulb bodies (other families: DEs, for scheduling)
-  uint32_t pix_body0 = 0;  // acc_body when the lane's pixel started
-#ifdef FRM_STAMPS
-  uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
-  uint64_t stamp_consume = 0, stamp_refill = 0, n_fetch = 0;
-  uint64_t stamp_sub[4] = {0, 0, 0, 0};  // consume: distance, primary, taps, shadow
-  const uint64_t stamp_begin = __builtin_amdgcn_s_memtime();
-  const uint64_t stamp_real0 = __builtin_amdgcn_s_memrealtime();
-#define FRM_SUB_BEGIN() const uint64_t sub0 = __builtin_amdgcn_s_memtime()
-#define FRM_SUB_END(k) stamp_sub[k] += __builtin_amdgcn_s_memtime() - sub0
-#else
-#define FRM_SUB_BEGIN()
-#define FRM_SUB_END(k)
-#endif
-
-  for (;;) {
-    // Body phase (Mandelbulb): one loop body per computing lane per iteration, until
-    // a.service_min lanes wait for a service pass (finished DE, or idle with work left)
-    // or no lane computes. The service pass costs the same however many lanes take part.
-    if constexpr (FAM == kMandelbulb) {
-      for (;;) {
-        const uint64_t busy = ballot(pix != kIdle && !done);
-        const uint32_t waiting = exhausted ? (uint32_t)__popcll(ballot(pix != kIdle && done))
-                                           : 64u - (uint32_t)__popcll(busy);
-        if (busy == 0 || waiting >= a.service_min) break;
-#ifdef FRM_STAMPS
-        n_loop++;
-#endif
-        if (pix != kIdle && !done) {
-          mb_step(su, q, mag, z, dr);
-          body++;
-          if (body > n_iter) {
-            done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
-          } else {
-            mag = mb_length(z);
-            done = mag > su.mb_bailout;
-          }
-        }
-      }
-    }
-
-    // Service pass.
-#ifdef FRM_STAMPS  // diagnostic build: wave cycles spent in service passes -> counters[7]
-    const uint64_t stamp0 = __builtin_amdgcn_s_memtime();
-#endif
-    // 1. consume finished DEs. Branch-light: the bookkeeping of every phase is computed for
-    //    every lane with selects; only the distance, the last-tap transition (normal, record,
-    //    shadow ray) and the record store of a finished pixel are branches.
-    const bool cons = pix != kIdle && done;
-    bool ev_bail = false;
-    if (cons) {
-      done = false;
-      if constexpr (FAM == kMandelbulb) {
-        FRM_SUB_BEGIN();
-        de = mb_distance(mag, dr);
-        acc_body += body;          // bodies this DE ran (N+1 on a count exit)
-        ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
-        FRM_SUB_END(0);
-      }
-    }
-    const bool ev_prim = cons && phase == kPrimary, ev_shadow = cons && phase == kShadow;
-    const bool tap = cons && !ev_prim && !ev_shadow;  // normal taps k.xyy, k.yyx, k.yxy, k.xxx
-    const bool hit = de <= kMinDistance;              // object_result.distance >= 0
-    const bool ev_hit = ev_prim && hit;
-    // shadow closeness = min(closeness, d / t) before t moves (d / 0 on step 0, as in
-    // fragment.wgsl:292); computed by every lane, kept by shadow lanes
-    const float cl = min_(closeness, de / t);
-    closeness = ev_shadow ? cl : closeness;
-    const bool step = (ev_prim || ev_shadow) && !hit;  // march on: t += d, it++
-    const float t_next = t + de;
-    const uint32_t it_next = it + 1u;
-    const bool more = it_next < f.max_steps && t_next < kMaxTotalDistance;
-    t = step ? t_next : t;
-    it = step ? it_next : it;
-    psteps = ev_hit ? it : psteps;
-    const bool fin = (step && !more) || (ev_shadow && hit);  // primary miss, or shadow march ends
-    const bool sun_miss = ev_shadow && step && !more;
-    bool need_point = ev_hit || (step && more) || tap;  // start a DE at the phase's next sample point
-    // tap k adds s_k * d to the sum (k = 0 sets it); s_0..s_3 = (+--), (--+), (-+-), (+++)
-    const uint32_t k = phase - kTap0;
-    const float dx = (k == 0u || k == 3u) ? de : -de, dy = (k >= 2u) ? de : -de,
-                dz = (k == 1u || k == 3u) ? de : -de;
-    // (component-wise: a select of whole structs compiles to a select of stack addresses)
-    const float sx = (k == 0u) ? dx : nsum.x + dx, sy = (k == 0u) ? dy : nsum.y + dy,
-                sz = (k == 0u) ? dz : nsum.z + dz;
-    nsum = mk(tap ? sx : nsum.x, tap ? sy : nsum.y, tap ? sz : nsum.z);
-    phase = ev_hit ? kTap0 : (tap ? phase + 1u : phase);  // after the last tap: kShadow
-    if (tap && k == kTap3 - kTap0) {  // normal, then the shadow ray toward the sun
-      FRM_SUB_BEGIN();
-      const v3 n = normalize(nsum);
-      const v3 hp = ray_at(o, t, d);
-      *reinterpret_cast<float4*>(&rec[pix].t) = make_float4(t, n.x, n.y, n.z);
-      o = shadow_origin(hp, n);
-      d = to_sun();
-      t = 0.f;
-      it = 0;
-      closeness = kInfinity;
-      FRM_SUB_END(2);
-    }
-    if (fin) {  // primary miss (flags 0: BACKGROUND_COLOR) or end of the shadow march
-      FRM_SUB_BEGIN();
-      const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
-      *reinterpret_cast<uint4*>(&rec[pix].closeness) =
-          make_uint4(__float_as_uint(closeness), psteps, flags, cost_key(acc_body - pix_body0));
-      pix = kIdle;
-      FRM_SUB_END(3);
-    }
-    // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
-#ifdef FRM_STAMPS
-    const uint64_t stamp1 = __builtin_amdgcn_s_memtime();
-    stamp_consume += stamp1 - stamp0;
-#endif
-    const uint64_t want = ballot(pix == kIdle);
-    if (want != 0 && !exhausted) {
-      if (slots_used == kChunk) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.queue, kChunk);
-        base = uniform(__shfl(base, 0, 64));
-#ifdef FRM_STAMPS
-        n_fetch++;
-#endif
-        if (base >= total) {
-          exhausted = true;
-#ifdef FRM_STAMPS
-          real_exhaust = __builtin_amdgcn_s_memrealtime();
-          if (lane == 0) atomicMin(a.debug + 2, (unsigned long long)real_exhaust);
-#endif
-        } else {
-          // the i-th pixel fetched is pixel_order[i]: most expensive first (the previous
-          // frame's cost keys, frm_sched.hip), row-major without history
-          uint32_t p = kIdle;
-          v3 ray = mk(0.f, 0.f, 0.f);
-          if (base + lane < total) {
-            p = a.pixel_order[base + lane];
-            const uint32_t lr = p / f.width, x = p - lr * f.width;
-            ray = camera_ray(f, x, band_row_to_global(a.g, lr));
-          }
-          n_pix += count(p != kIdle);
-          chunk_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
-          __builtin_amdgcn_wave_barrier();
-          slots_used = 0;
-        }
-      }
-      if (slots_used < kChunk) {
-        const uint32_t slot = slots_used + __popcll(want & (lane_bit - 1ull));
-        if ((want & lane_bit) && slot < kChunk) {
-          const float4 r = chunk_rays[wave][slot];
-          pix = __float_as_uint(r.w);
-          if (pix != kIdle) {
-            pix_body0 = acc_body;
-            d = mk(r.x, r.y, r.z);
-            o = f.origin;
-            t = 0.f;
-            it = 0;
-            phase = kPrimary;
-            need_point = true;
-          }
-        }
-        slots_used = min(kChunk, slots_used + (uint32_t)__popcll(want));
-      }
-    }
-
-#ifdef FRM_STAMPS
-    stamp_refill += __builtin_amdgcn_s_memtime() - stamp1;
-#endif
-    // 3. start the next DE of every lane that needs one (the hit point of the normal
-    //    taps is recomputed from the unchanged primary ray: ray_at(o, t_hit, d))
-    if (need_point) {
-      const v3 r = ray_at(o, t, d);
-      // normal tap k samples r + s_k * MIN_DISTANCE (normal_tap_pos), with selects
-      const uint32_t kq = phase - kTap0;
-      const bool is_tap = kq <= kTap3 - kTap0;
-      const float e = kMinDistance;
-      const float ex = (kq == 0u || kq == 3u) ? e : -e, ey = (kq >= 2u) ? e : -e, ez = (kq == 1u || kq == 3u) ? e : -e;
-      q = mk(is_tap ? r.x + ex : r.x, is_tap ? r.y + ey : r.y, is_tap ? r.z + ez : r.z);
-      if constexpr (FAM == kMandelbulb) {
-        z = q;
-        dr = 1.f;
-        body = 0;
-        mag = mb_length(q);
-        done = mag > su.mb_bailout;
-      } else {
-        DeCount unused = {0u, 0u};
-        de = scene_de<FAM, ITERS>(su, q, unused);
-        done = true;
-        acc_body++;  // fixed-trip families: the scheduling cost unit is one DE
-      }
-    }
-
-    n_prim += count(ev_prim);
-    n_hit += count(ev_hit);
-    n_shadow += count(ev_shadow);
-    n_bail += count(ev_bail);
-#ifdef FRM_STAMPS
-    stamp_service += __builtin_amdgcn_s_memtime() - stamp0;
-    n_service++;
-#endif
-
-    if (exhausted && ballot(pix != kIdle) == 0) break;
-  }
-
-  if constexpr (FAM == kMandelbulb) n_body = wave_sum(acc_body);
-#ifdef FRM_STAMPS
-  if (lane == 0) {
-    atomicAdd(&a.counters[7], (unsigned long long)stamp_service);
-    atomicAdd(a.debug, (unsigned long long)(__builtin_amdgcn_s_memtime() - stamp_begin));
-    atomicAdd(a.debug + 1, (unsigned long long)n_service);
-    atomicMin(a.debug + 3, (unsigned long long)stamp_real0);  // first wave start (100 MHz)
-    atomicMax(a.debug + 4, (unsigned long long)__builtin_amdgcn_s_memrealtime());  // last wave end
-  }
-  {
-    const uint32_t w = blockIdx.x * 4u + wave;
-    uint32_t hw = 0;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    if (lane == 0 && w < kWaveDebugSlots) {
-      unsigned long long* r = g_wave_debug + 16u * w;
-      r[8] = stamp_consume;
-      r[9] = stamp_refill;
-      r[10] = n_fetch;
-      for (int k = 0; k < 4; ++k) r[11 + k] = stamp_sub[k];
-      r[0] = n_loop;
-      r[1] = n_body;
-      r[2] = n_service;
-      r[3] = stamp_service;
-      r[4] = __builtin_amdgcn_s_memtime() - stamp_begin;
-      r[5] = stamp_real0;
-      r[6] = real_exhaust;
-      r[7] = ((unsigned long long)hw << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - stamp_real0);
-    }
-  }
-#endif
-  if (lane == 0) {
-    unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-      if (v[k]) atomicAdd(&a.counters[k], v[k]);
-  }
-}
-
-// Coherent shading of the records written by march_persistent: fragment.wgsl:333-348
-// (+ the Rgba8UnormSrgb store). One thread per local pixel, row-major.
-template <uint32_t FAM>
-__global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
-  __shared__ float table[256];
-  table[threadIdx.x] = kSrgbThresholds[threadIdx.x];
-  __syncthreads();
-  const uint32_t width = a.f.width;
-  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
-  if (idx >= a.g.local_rows * width) return;
-  const uint32_t lr = idx / width, x = idx - lr * width;
-  const uint32_t y = band_row_to_global(a.g, lr);
-  if (y >= a.f.height) return;
-  const uint4 r1 = *reinterpret_cast<const uint4*>(&a.records[idx].closeness);
-  if (a.pixel_key) a.pixel_key[idx] = (uint8_t)r1.w;  // coalesced, for the next frame's order
-  uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
-  if (r1.z & kRecHit) {
-    const float4 r0 = *reinterpret_cast<const float4*>(&a.records[idx].t);
-    const v3 dir = camera_ray(a.f, x, y);
-    const v3 hp = ray_at(a.f.origin, r0.x, dir);
-    const v3 n = mk(r0.y, r0.z, r0.w);
-    float spec;
-    v3 color = shade_hit_pre(a.f, scene_color<FAM>(hp), dir, n, r1.y, &spec);
-    color = shade_hit_post(color, spec, (r1.z & kRecSunMiss) ? -kInfinity : 0.0f, __uint_as_float(r1.x));
-    word = pack_rgba(color, table);
-  }
-  a.out[idx] = word;
-}
-
-// dst row y <- band b = y / band_rows, held by rank b % ranks as its (b / ranks)-th band.
-// T = uint4 when rows and rank strides are 16-byte multiples, else uint32_t.
 template <typename T>
 __global__ __launch_bounds__(256) void unshuffle_bands(const T* __restrict__ src, size_t rank_stride,
                                                        T* __restrict__ dst, uint32_t row_words,
@@ -480,37 +104,54 @@ hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, 
   return hipGetLastError();
 }
 
+static int blocks_override() {  // experiments: FRM_BLOCKS_PER_CU
+  const char* env = getenv("FRM_BLOCKS_PER_CU");
+  const int v = env ? atoi(env) : 0;
+  return v >= 1 && v <= 16 ? v : 0;
+}
+
+// A reloaded module's kernel (frm_reload.hip) takes the same KernelArgs by value.
+static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStream_t stream, const KernelArgs& args) {
+  void* params[] = {const_cast<KernelArgs*>(&args)};
+  return hipModuleLaunchKernel(fn, grid.x, grid.y, grid.z, block.x, block.y, block.z, 0, stream, params, nullptr);
+}
+
 template <uint32_t FAM, bool ITERS>
-static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStream_t stream) {
+static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStream_t stream,
+                                    const ReloadedKernels* rk) {
   static int blocks_per_cu = 0;  // occupancy of this instantiation (per process)
   if (blocks_per_cu == 0) {
     int n = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS>, 256, 0);
     if (e != hipSuccess) return e;
     blocks_per_cu = n > 0 ? n : 1;
-    if (const char* env = getenv("FRM_BLOCKS_PER_CU")) {  // experiments
-      const int v = atoi(env);
-      if (v >= 1 && v <= 16) blocks_per_cu = v;
-    }
   }
+  int bpc = rk ? rk->persistent_blocks_per_cu[FAM][ITERS] : blocks_per_cu;
+  if (const int v = blocks_override()) bpc = v;
   // every wave starts with one chunk of 64 pixels; never launch more waves than chunks
-  uint32_t blocks = (uint32_t)(blocks_per_cu * cu_count);
+  uint32_t blocks = (uint32_t)(bpc * cu_count);
   const uint32_t max_blocks = ((args.npix + kChunk - 1u) / kChunk + 3u) / 4u;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(256), 0, stream, args);
   const uint32_t pixels = args.g.local_rows * args.f.width;
+  if (rk) {
+    hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(256), stream, args);
+    if (e != hipSuccess) return e;
+    return module_launch(rk->shade[FAM], dim3((pixels + 255u) / 256u), dim3(256), stream, args);
+  }
+  hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(256), 0, stream, args);
   hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u), dim3(256), 0, stream, args);
   return hipGetLastError();
 }
 
 template <uint32_t FAM>
-static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_count,
-                                hipStream_t stream) {
+static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
+                                const ReloadedKernels* rk) {
   if (kind == kKernelPersistent)
-    return args.s.n ? launch_persistent<FAM, true>(args, cu_count, stream)
-                    : launch_persistent<FAM, false>(args, cu_count, stream);
+    return args.s.n ? launch_persistent<FAM, true>(args, cu_count, stream, rk)
+                    : launch_persistent<FAM, false>(args, cu_count, stream, rk);
   dim3 grid((args.f.width + 15u) / 16u, (args.g.local_rows + 15u) / 16u);
+  if (rk) return module_launch(rk->simple[FAM][args.s.n ? 1 : 0], grid, dim3(256), stream, args);
   if (args.s.n)
     hipLaunchKernelGGL((render_simple<FAM, true>), grid, dim3(256), 0, stream, args);
   else
@@ -518,13 +159,14 @@ static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_
   return hipGetLastError();
 }
 
-hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream) {
+hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
+                         const ReloadedKernels* rk) {
   switch (args.s.family) {
-    case kMenger: return launch_family<kMenger>(args, kind, cu_count, stream);
-    case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream);
-    case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream);
-    case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream);
-    default: return launch_family<kSphere>(args, kind, cu_count, stream);
+    case kMenger: return launch_family<kMenger>(args, kind, cu_count, stream, rk);
+    case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream, rk);
+    case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream, rk);
+    case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream, rk);
+    default: return launch_family<kSphere>(args, kind, cu_count, stream, rk);
   }
 }
 

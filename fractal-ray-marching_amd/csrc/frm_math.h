@@ -18,12 +18,16 @@
 // Compile with -ffp-contract=off on both host and device: every fusion below is an
 // explicit fma.
 #pragma once
+#if !defined(__HIPCC_RTC__)  // hiprtc (frm_reload) provides these itself
 #include <stdint.h>
 #include <string.h>
 #include <math.h>
+#endif
 
 #if defined(__HIPCC__) || defined(__HIP__)
+#if !defined(__HIPCC_RTC__)
 #include <hip/hip_runtime.h>
+#endif
 #define FRM_HD __host__ __device__ __forceinline__
 #else
 #define FRM_HD static inline

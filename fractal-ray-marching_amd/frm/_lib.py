@@ -19,6 +19,7 @@ FRM_ERR_OUT_OF_MEMORY = 4
 FRM_ERR_NOT_READY = 5
 FRM_ERR_BUFFER_TOO_SMALL = 6
 FRM_ERR_UNSUPPORTED = 7
+FRM_ERR_COMPILE = 8
 
 FRM_NUM_SCENES = 19
 FRM_DEFAULT_MAX_STEPS = 5000
@@ -105,6 +106,7 @@ SIGNATURES = [
     ("frm_render", ctypes.c_int, [ctypes.c_void_p, _P(FrmStats)]),
     ("frm_read_frame", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_synchronize", ctypes.c_int, [ctypes.c_void_p]),
+    ("frm_reload", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     ("frm_present", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_band_rows_for", ctypes.c_int,

@@ -3,6 +3,7 @@ API (src/graphics.rs): init -> resize -> update_parameters_buffer -> render ->
 (read_frame replaces the blit+present). Errors raise FrmError; nothing falls back to
 the CPU."""
 import ctypes
+import os
 
 import numpy as np
 
@@ -72,6 +73,22 @@ class Renderer:
 
     def synchronize(self):
         self._check(self._lib.frm_synchronize(self.ctx))
+
+    # graphics.rs:44-48 (reload): recompile the render kernels from an edited copy of csrc/
+    # (hiprtc); raises FrmError (FRM_ERR_COMPILE + compiler log) and keeps the previous
+    # kernels on failure. source_dir=None returns to the built-in kernels.
+    def reload(self, source_dir):
+        arg = None if source_dir is None else os.fsencode(source_dir)
+        self._check(self._lib.frm_reload(self.ctx, arg))
+
+    # graphics.rs:39-43 (try_reload): print the error instead of raising
+    def try_reload(self, source_dir):
+        try:
+            self.reload(source_dir)
+            return True
+        except _lib.FrmError as e:
+            print(e)
+            return False
 
     # multi-GPU row tiling (device pointers, e.g. torch tensors' data_ptr())
     def render_bands(self, dev_ptr, nbytes, band_rows, first_band, band_stride, stream=0,

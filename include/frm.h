@@ -23,8 +23,10 @@
 #ifndef FRM_H
 #define FRM_H
 
+#if !defined(__HIPCC_RTC__) /* hiprtc (frm_reload) defines the fixed-width types itself */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -41,7 +43,8 @@ enum {
   FRM_ERR_OUT_OF_MEMORY = 4,    /* device allocation failed                           */
   FRM_ERR_NOT_READY = 5,        /* frm_render before frm_resize / frm_set_parameters  */
   FRM_ERR_BUFFER_TOO_SMALL = 6, /* destination smaller than the frame or band set      */
-  FRM_ERR_UNSUPPORTED = 7       /* e.g. num_iterations above FRM_MAX_NUM_ITERATIONS    */
+  FRM_ERR_UNSUPPORTED = 7,      /* e.g. num_iterations above FRM_MAX_NUM_ITERATIONS    */
+  FRM_ERR_COMPILE = 8           /* frm_reload: the sources failed to compile (log in last_error) */
 };
 
 /* ---- the reference's uniform, byte for byte -------------------------------
@@ -60,7 +63,9 @@ typedef struct frm_parameters {
   uint8_t padding[12];
 } frm_parameters;
 
-#ifdef __cplusplus
+#if defined(__HIPCC_RTC__)
+static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
+#elif defined(__cplusplus)
 static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
 static_assert(offsetof(frm_parameters, aspect_scale) == 64, "aspect_scale @64");
 static_assert(offsetof(frm_parameters, time) == 72, "time @72");
@@ -147,6 +152,15 @@ int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes);
 int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags, uint8_t* dst,
                 size_t dst_bytes);
 int frm_synchronize(frm_ctx* ctx);
+
+/* Runtime kernel reload (the reference's `r` key: graphics.rs:39-48, reloadable_graphics.rs:
+ * 15-52). Recompiles the render kernels with hiprtc from source_dir, a directory holding an
+ * edited copy of this package's csrc/ headers (frm_render_kernels.h and the headers it
+ * includes: scenes, distance estimators, builtins, shading), and renders every later frame
+ * of this context with them. On failure (FRM_ERR_COMPILE, log in frm_last_error) the
+ * previous kernels stay active, as the reference keeps its pipeline. source_dir = NULL
+ * returns to the built-in kernels. Waits for the context's stream. */
+int frm_reload(frm_ctx* ctx, const char* source_dir);
 
 /* ---- row-tiled rendering for multi-GPU (no reference counterpart: the reference
  *      is single-device). Band b covers frame rows [b*band_rows, (b+1)*band_rows).

@@ -8,5 +8,5 @@ mkdir -p variants
 make -s OBJDIR=build/obj_$NAME EXTRA_HIPFLAGS="$FLAGS" build/obj_$NAME/frm_kernels.o build/obj_$NAME/frm_api.o \
   build/obj_$NAME/frm_sched.o build/obj_$NAME/frm_host.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o variants/$NAME.so build/obj_$NAME/frm_kernels.o \
-  build/obj_$NAME/frm_api.o build/obj_$NAME/frm_sched.o build/obj_$NAME/frm_host.o
+  build/obj_$NAME/frm_api.o build/obj_$NAME/frm_sched.o build/obj_$NAME/frm_host.o build/obj_$NAME/frm_reload.o -lhiprtc
 echo "variants/$NAME.so"
