@@ -3,9 +3,16 @@
 
 Workload (BASELINE.json metric): 3840x2160 Mandelbulb (scene 18 at power 8), 12 DE
 iterations, 256 march steps, fixed camera pose P1; one "step" = one whole frame of the
-hot path (fragment_main for every pixel) with inputs resident on the GPU. N GPUs
-row-tile the same frame (interleaved bands, strong scaling) and gather it to rank 0
-over RCCL, then rank 0 reassembles it (frm_unshuffle_bands).
+hot path (fragment_main for every pixel) with inputs resident on the GPU.
+
+N GPUs (one process each, torch.distributed.run):
+* --split frames (default): alternate-frame rendering. Frames are independent units, so
+  each rank renders whole frames of the same workload, seen from the base pose rotated
+  about +y by rank * pi/4 (an orbit fly-through; rank 0 = the base pose). There is no
+  data-path collective and per-GPU work is fixed, so scaling is "weak".
+* --split rows: one frame split into interleaved row bands across the ranks, gathered to
+  rank 0 over RCCL and reassembled there (frm_unshuffle_bands): strong scaling, limited
+  by the longest pixel's sequential march.
 
 Prints ONE JSON line on rank 0. `value` = G ray-march-steps/s of the whole job
 (primary + shadow march() iterations, counted exactly by the kernel, / wall time).
@@ -14,6 +21,7 @@ Prints ONE JSON line on rank 0. `value` = G ray-march-steps/s of the whole job
                     [--pose P0|P1|P2] [--kernel persistent|simple] [--no-cpu-baseline]
 """
 import argparse
+import math
 import json
 import os
 import sys
@@ -40,6 +48,10 @@ def parse():
     ap.add_argument("--pose", default="P1")
     ap.add_argument("--kernel", default="persistent", choices=["persistent", "simple"])
     ap.add_argument("--band-rows", type=int, default=0)
+    ap.add_argument("--split", default="frames", choices=["frames", "rows"],
+                    help="N>1: 'frames' = alternate-frame rendering, each rank renders whole frames of "
+                    "an orbit fly-through (no data-path collective, weak scaling); 'rows' = one frame "
+                    "split into interleaved row bands + RCCL gather to rank 0 (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
@@ -114,12 +126,28 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N>1 with torch.distributed.run)")
+    # test hooks for a 1-GPU box: every rank on device 0, and gloo (RCCL refuses two ranks
+    # on one GPU); the driver's multi-GPU runs use neither
+    if os.environ.get("FRM_BENCH_SHARED_DEVICE"):
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("FRM_BENCH_BACKEND") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     w = frm.WORKLOADS[args.workload]
     params = frm.make_parameters(w, pose=args.pose)
+    afr = world > 1 and args.split == "frames"
+    if afr and rank > 0:
+        # alternate-frame rendering: rank r renders the view of the same workload from the
+        # pose rotated about +y by r * pi/4 (an orbit fly-through, looking at the same
+        # point as the base pose; rank 0 renders the base pose itself)
+        (x, y, z), yaw, pitch = frm.POSES[args.pose]
+        a = rank * math.pi / 4
+        cam = frm.Camera((math.cos(a) * x + math.sin(a) * z, y, -math.sin(a) * x + math.cos(a) * z), yaw + a, pitch)
+        params.update_camera(cam)
     flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
         frm.FRM_FLAG_SIMPLE_KERNEL if args.kernel == "simple" else 0)
     r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags)
@@ -128,7 +156,8 @@ def main():
     if args.reload:
         r.reload(args.reload)
 
-    band_rows = args.band_rows or (w.height if world == 1 else tiling.choose_band_rows(w.height, world))
+    split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
+    band_rows = args.band_rows or (w.height if split == 1 else tiling.choose_band_rows(w.height, world))
     dev = torch.device("cuda", local)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     # A dedicated stream: its handle is non-null, so libfrm launches on it (a NULL handle
@@ -152,7 +181,7 @@ def main():
         r.unshuffle_bands(gathered.data_ptr(), gathered.numel() // world, frame.data_ptr(), frame.numel(),
                           band_rows, world, stream.cuda_stream)
 
-    tf = RowTiledFrame(w.width, w.height, rank, world, band_rows, dev, render_bands, unshuffle)
+    tf = RowTiledFrame(w.width, w.height, 0 if split == 1 else rank, split, band_rows, dev, render_bands, unshuffle)
 
     # Animated workloads (C5): every frame advances time by 1/60 s through the reference's
     # Timing::update (frm_timing_update), as the reference's frame loop does
@@ -206,7 +235,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if split > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: deterministic Parameters (fixed camera pose, fixed time), no input data",
@@ -215,11 +244,13 @@ def main():
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
                 "pose": args.pose, "kernel": args.kernel + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
-                "parallelism": f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if world > 1
-                               else "single GPU",
+                "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if split > 1 else
+                                f"alternate-frame rendering x{world}: rank r renders the {args.pose} view "
+                                f"rotated by r*pi/4 about +y, whole frames, no data-path collective"
+                                if world > 1 else "single GPU"),
             },
-            "frames_per_sec": args.steps / elapsed,
-            "march_steps_per_frame": steps_total / args.steps,
+            "frames_per_sec": args.steps * (world if split == 1 else 1) / elapsed,
+            "march_steps_per_frame": steps_total / args.steps / (world if split == 1 else 1),
             "roofline": {
                 "bound": "valu",
                 "achieved": achieved,
