@@ -138,25 +138,33 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     // a.service_min lanes wait for a service pass (finished DE, or idle with work left)
     // or no lane computes. The service pass costs the same however many lanes take part.
     if constexpr (FAM == kMandelbulb) {
+      // The loop keeps its lane sets as wave-uniform masks (SGPRs): `pending` predicates the
+      // body directly (inverse ballot -> exec) and one ballot per iteration retires lanes,
+      // instead of a per-lane flag merged under exec masks every iteration.
+      const uint64_t live = ballot(pix != kIdle);
+      uint64_t pending = live & ~ballot(done);
+      // lanes that count as waiting when not pending: finished DEs, and idle lanes while
+      // the queue still has pixels
+      const uint64_t waitable = exhausted ? live : ~0ull;
       for (;;) {
-        const uint64_t busy = ballot(pix != kIdle && !done);
-        const uint32_t waiting = exhausted ? (uint32_t)__popcll(ballot(pix != kIdle && done))
-                                           : 64u - (uint32_t)__popcll(busy);
-        if (busy == 0 || waiting >= a.service_min) break;
+        if (pending == 0 || (uint32_t)__popcll(waitable & ~pending) >= a.service_min) break;
 #ifdef FRM_STAMPS
         n_loop++;
 #endif
-        if (pix != kIdle && !done) {
+        uint32_t fin = 0;
+        if (lane_in(pending)) {
           mb_step(su, q, mag, z, dr);
           body++;
           if (body > n_iter) {
-            done = true;  // N+1 bodies: the distance uses the last loop-top magnitude
+            fin = 1;  // N+1 bodies: the distance uses the last loop-top magnitude
           } else {
             mag = mb_length(z);
-            done = mag > su.mb_bailout;
+            fin = mag > su.mb_bailout;
           }
         }
+        pending &= ~ballot(fin != 0);
       }
+      done = !lane_in(pending);  // idle lanes: masked by cons
     }
 
     // Service pass.

@@ -198,6 +198,16 @@ __device__ __forceinline__ uint64_t ballot(bool b) {
   return b;
 #endif
 }
+// This lane's bit of a wave-uniform lane mask. The inverse ballot makes the mask the exec
+// predicate directly (no VALU); older compilers (the ROCm 7.0 hiprtc bundled with torch,
+// used by frm_reload) lack it and test the bit.
+__device__ __forceinline__ bool lane_in(uint64_t mask) {
+#if defined(__HIP_DEVICE_COMPILE__) && __has_builtin(__builtin_amdgcn_inverse_ballot_w64)
+  return __builtin_amdgcn_inverse_ballot_w64(mask);
+#else
+  return (mask >> (threadIdx.x & 63u)) & 1u;
+#endif
+}
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
