@@ -103,9 +103,15 @@ __device__ __forceinline__ float acos_dev(float t) {
 // atan2_ for tame x, y (each 0 or with magnitude in [2^-60, 2^40]).
 __device__ __forceinline__ float atan2_tame(float y, float x) {
   float ax = fabsf(x), ay = fabsf(y);
-  float mx = max_(ax, ay), mn = min_(ax, ay);
-  float a = div_tame_nz(mn, mx);  // mn >= +0
-  a = (mx == 0.0f) ? 0.0f : a;
+  // mx = max_(ax, ay, 2^-100), mn = min_(ax, ay) for finite x, y: plain v_max3 / v_min with
+  // |.| source modifiers, without the NaN-quieting canonicalizes the compiler adds to
+  // fmaxf / fminf in IEEE mode (same values for non-NaN operands). Tame non-zero
+  // magnitudes are >= 2^-60, so the 2^-100 floor only replaces mx = 0 (x = y = 0), where
+  // the Newton division then gives 0 / 2^-100 = +0: the value atan2's a = 0 branch needs.
+  float mx, mn;
+  asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(mx) : "v"(x), "v"(y), "s"(0x1p-100f));
+  asm("v_min_f32 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
+  const float a = div_tame_nz(mn, mx);  // mn >= +0
   float s = a * a;
   float q = fma_(fma_(fma_(fma_(fma_(fma_(fma_(0.002974590389872539f, s, -0.016581183968493302f), s,
                                       0.04355353931255974f), s, -0.07580578130128461f), s,

@@ -123,7 +123,10 @@ def _fast_inputs(name, rng):
     if name == "acos_dev":
         return "acos", np.concatenate([rng.uniform(-1, 1, n), [1, -1, 0.5, -0.5, 0.0, -0.0, 1.0000001, np.nan]]), None
     if name == "atan2_tame":
-        return "atan2", _tame(rng, n), _tame(rng, n)
+        # + signed-zero pairs (x = y = 0: the 2^-100 floor of mx) and the range edges
+        edge = np.array([0.0, -0.0, 2.0 ** -60, -(2.0 ** -60), 2.0 ** 40, -(2.0 ** 40), 1.0])
+        ey, ex = (g.ravel() for g in np.meshgrid(edge, edge))
+        return "atan2", np.concatenate([_tame(rng, n), ey]), np.concatenate([_tame(rng, n), ex])
     if name == "log2_tame":
         return "log2", np.concatenate([np.exp2(rng.uniform(-126, 128, n)), [1.0, 2.0 ** -126, 0.7071067]]), None
     # exp2_tame: finite y in [-400, 128]
