@@ -11,7 +11,7 @@ import json
 import sys
 
 
-KERNEL = "render"
+KERNEL = "march_persistent"
 
 
 def load(d, name):
