@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="HEADLINE")
     ap.add_argument("--pose", default="P1")
-    ap.add_argument("--kernel", default="persistent", choices=["persistent", "simple"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "persistent", "simple"],
+                    help="auto: libfrm's choice (simple below one resident persistent grid of pixels)")
     ap.add_argument("--band-rows", type=int, default=0)
     ap.add_argument("--split", default="frames", choices=["frames", "rows"],
                     help="N>1: 'frames' = alternate-frame rendering, each rank renders whole frames of "
@@ -149,7 +150,7 @@ def main():
         cam = frm.Camera((math.cos(a) * x + math.sin(a) * z, y, -math.sin(a) * x + math.cos(a) * z), yaw + a, pitch)
         params.update_camera(cam)
     flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
-        frm.FRM_FLAG_SIMPLE_KERNEL if args.kernel == "simple" else 0)
+        {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel])
     r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags)
     r.resize(w.width, w.height)
     r.update_parameters_buffer(params)
@@ -158,6 +159,8 @@ def main():
 
     split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
     band_rows = args.band_rows or (w.height if split == 1 else tiling.choose_band_rows(w.height, world))
+    local_pixels = w.width * min(w.height, tiling.rank_rows(w.height, band_rows, 0 if split == 1 else rank, split))
+    kernel_used = r.kernel_for(local_pixels) + (" (auto)" if args.kernel == "auto" else "")
     dev = torch.device("cuda", local)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     # A dedicated stream: its handle is non-null, so libfrm launches on it (a NULL handle
@@ -242,7 +245,7 @@ def main():
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
-                "pose": args.pose, "kernel": args.kernel + (" (runtime-compiled)" if args.reload else ""),
+                "pose": args.pose, "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if split > 1 else
                                 f"alternate-frame rendering x{world}: rank r renders the {args.pose} view "

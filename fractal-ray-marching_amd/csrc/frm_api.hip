@@ -21,6 +21,11 @@ using namespace frm;
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
 static constexpr uint32_t kDefaultServiceMin = 20;  // swept 16..36 on MI355X (round 1): flat 16-24
+// Kernel choice without a FRM_FLAG_*_KERNEL flag: below one resident persistent grid
+// (6 blocks of 256 lanes per CU for the Mandelbulb) a launch has fewer pixels than lanes,
+// and the persistent kernel's fixed costs (pixel sort, grid, separate shading pass) outweigh
+// its load balancing: 256x256 runs 23 G steps/s simple vs 10 persistent, 1920x1080 8 vs 20.
+static constexpr uint64_t kSimplePixelsPerCu = 1536;
 
 struct frm_ctx {
   int device = 0;
@@ -125,9 +130,15 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   return a;
 }
 
+KernelKind kernel_for(const frm_ctx* ctx, uint64_t pixels) {
+  if (ctx->flags & FRM_FLAG_SIMPLE_KERNEL) return kKernelSimple;
+  if (ctx->flags & FRM_FLAG_PERSISTENT_KERNEL) return kKernelPersistent;
+  return pixels < kSimplePixelsPerCu * (uint64_t)ctx->cu_count ? kKernelSimple : kKernelPersistent;
+}
+
 int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
   if (a.g.local_rows == 0) return FRM_OK;
-  KernelKind kind = (ctx->flags & FRM_FLAG_SIMPLE_KERNEL) ? kKernelSimple : kKernelPersistent;
+  const KernelKind kind = kernel_for(ctx, a.npix);
   if (kind == kKernelPersistent) {
     const size_t need = (size_t)a.g.local_rows * a.f.width;
     if (need > ctx->records_cap) {  // grows outside the steady state (first frame of a size)
@@ -205,6 +216,10 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   if (!out_ctx || !config) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "out_ctx/config is NULL");
   *out_ctx = nullptr;
   if (config->reserved != 0) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.reserved must be 0");
+  const uint32_t kernels = FRM_FLAG_SIMPLE_KERNEL | FRM_FLAG_PERSISTENT_KERNEL;
+  if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE)) || (config->flags & kernels) == kernels)
+    return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.flags 0x%x: unknown flag or both kernel flags",
+                config->flags);
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n == 0)
@@ -375,6 +390,12 @@ int frm_synchronize(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return FRM_OK;
+}
+
+int frm_kernel_for_pixels(const frm_ctx* ctx, uint64_t pixels, uint32_t* out_kernel) {
+  if (!ctx || !out_kernel) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx/out_kernel is NULL");
+  *out_kernel = kernel_for(ctx, pixels) == kKernelSimple ? FRM_KERNEL_SIMPLE : FRM_KERNEL_PERSISTENT;
   return FRM_OK;
 }
 

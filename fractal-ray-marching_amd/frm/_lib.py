@@ -27,6 +27,9 @@ FRM_MAX_NUM_ITERATIONS = 4096
 FRM_NUM_COUNTERS = 8
 FRM_FLAG_SCENE_SPHERE = 0x1
 FRM_FLAG_SIMPLE_KERNEL = 0x2
+FRM_FLAG_PERSISTENT_KERNEL = 0x4
+FRM_KERNEL_PERSISTENT = 0
+FRM_KERNEL_SIMPLE = 1
 FRM_BLIT_SRGB = 0x1
 FRM_BLIT_BGRA = 0x2
 
@@ -106,6 +109,7 @@ SIGNATURES = [
     ("frm_render", ctypes.c_int, [ctypes.c_void_p, _P(FrmStats)]),
     ("frm_read_frame", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_synchronize", ctypes.c_int, [ctypes.c_void_p]),
+    ("frm_kernel_for_pixels", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]),
     ("frm_reload", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     ("frm_present", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),

@@ -74,6 +74,12 @@ class Renderer:
     def synchronize(self):
         self._check(self._lib.frm_synchronize(self.ctx))
 
+    def kernel_for(self, pixels):
+        """'persistent' or 'simple': the kernel a launch of `pixels` pixels runs here."""
+        k = ctypes.c_uint32()
+        self._check(self._lib.frm_kernel_for_pixels(self.ctx, int(pixels), ctypes.byref(k)))
+        return "simple" if k.value == _lib.FRM_KERNEL_SIMPLE else "persistent"
+
     # graphics.rs:44-48 (reload): recompile the render kernels from an edited copy of csrc/
     # (hiprtc); raises FrmError (FRM_ERR_COMPILE + compiler log) and keeps the previous
     # kernels on failure. source_dir=None returns to the built-in kernels.

@@ -86,6 +86,14 @@ _Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
                                        the reference (its out-of-range scene ids map to 0). */
 #define FRM_FLAG_SIMPLE_KERNEL 0x2u /* use the one-thread-per-pixel kernel instead of the
                                        persistent ray-regeneration kernel (same bytes). */
+#define FRM_FLAG_PERSISTENT_KERNEL 0x4u /* always use the persistent kernel. With neither
+                                       kernel flag the context picks per launch: simple
+                                       below one resident persistent grid of pixels
+                                       (frm_kernel_for_pixels), persistent above. */
+
+/* kernels (frm_kernel_for_pixels) */
+#define FRM_KERNEL_PERSISTENT 0u
+#define FRM_KERNEL_SIMPLE 1u
 
 typedef struct frm_config {
   int32_t device;     /* HIP device ordinal (replaces the wgpu adapter request,
@@ -152,6 +160,12 @@ int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes);
 int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags, uint8_t* dst,
                 size_t dst_bytes);
 int frm_synchronize(frm_ctx* ctx);
+
+/* The kernel (FRM_KERNEL_*) a render or band launch of `pixels` pixels runs on this
+ * context: the FRM_FLAG_*_KERNEL flag when set, otherwise FRM_KERNEL_SIMPLE when pixels
+ * is below one resident persistent grid (1536 lanes per CU) and FRM_KERNEL_PERSISTENT
+ * from there on. No reference counterpart (the reference has one fragment pipeline). */
+int frm_kernel_for_pixels(const frm_ctx* ctx, uint64_t pixels, uint32_t* out_kernel);
 
 /* Runtime kernel reload (the reference's `r` key: graphics.rs:39-48, reloadable_graphics.rs:
  * 15-52). Recompiles the render kernels with hiprtc from source_dir, a directory holding an

@@ -21,9 +21,9 @@ def local_rows(height, band_rows, first, stride):
 
 
 @pytest.mark.parametrize("width,height,band_rows,ranks,kernel_flags", [
-    (200, 118, 8, 3, 0),                            # 15 bands, the last one 6 rows
-    (131, 77, 5, 2, 0),                             # odd width, last band 2 rows
-    (96, 54, 54, 2, 0),                             # one band: rank 1 renders nothing
+    (200, 118, 8, 3, frm.FRM_FLAG_PERSISTENT_KERNEL),  # 15 bands, the last one 6 rows
+    (131, 77, 5, 2, frm.FRM_FLAG_PERSISTENT_KERNEL),   # odd width, last band 2 rows
+    (96, 54, 54, 2, frm.FRM_FLAG_PERSISTENT_KERNEL),   # one band: rank 1 renders nothing
     (200, 118, 8, 3, frm.FRM_FLAG_SIMPLE_KERNEL),
 ])
 def test_bands_reassemble_to_oracle_frame(gpu_renderer_factory, oracle, width, height, band_rows, ranks,

@@ -25,7 +25,7 @@ def counters_of(st):
             st["normal_evals"], st["fractal_bodies"], st["fractal_bailouts"], 0]
 
 
-@pytest.mark.parametrize("kernel_flags", [0, frm.FRM_FLAG_SIMPLE_KERNEL], ids=["persistent", "simple"])
+@pytest.mark.parametrize("kernel_flags", [frm.FRM_FLAG_PERSISTENT_KERNEL, frm.FRM_FLAG_SIMPLE_KERNEL], ids=["persistent", "simple"])
 @pytest.mark.parametrize("scene", SCENES)
 def test_all_scenes_bit_exact(gpu_renderer_factory, oracle, scene, kernel_flags):
     for iters, time in ((0, 0.0), (3, 3.2175055), (6, 1.0)):
@@ -37,7 +37,7 @@ def test_all_scenes_bit_exact(gpu_renderer_factory, oracle, scene, kernel_flags)
         assert counters_of(st) == [int(c) for c in ref["counters"]]
 
 
-@pytest.mark.parametrize("kernel_flags", [0, frm.FRM_FLAG_SIMPLE_KERNEL], ids=["persistent", "simple"])
+@pytest.mark.parametrize("kernel_flags", [frm.FRM_FLAG_PERSISTENT_KERNEL, frm.FRM_FLAG_SIMPLE_KERNEL], ids=["persistent", "simple"])
 def test_headline_mandelbulb_bit_exact(gpu_renderer_factory, oracle, kernel_flags):
     for pose in ("P0", "P1", "P2"):
         p = params_for(18, 12, frm.POWER8_TIME, 192, 108, pose=pose)
@@ -47,25 +47,27 @@ def test_headline_mandelbulb_bit_exact(gpu_renderer_factory, oracle, kernel_flag
         assert counters_of(st) == [int(c) for c in ref["counters"]]
 
 
-def test_sphere_extension_c1(gpu_renderer_factory, oracle):
+@pytest.mark.parametrize("kernel_flags", [0, frm.FRM_FLAG_PERSISTENT_KERNEL], ids=["auto", "persistent"])
+def test_sphere_extension_c1(gpu_renderer_factory, oracle, kernel_flags):
     p = params_for(0, 0, 0.0, 256, 256)
-    img, st = gpu_render(gpu_renderer_factory, p, 256, 256, 64, frm.FRM_FLAG_SCENE_SPHERE)
+    img, st = gpu_render(gpu_renderer_factory, p, 256, 256, 64, frm.FRM_FLAG_SCENE_SPHERE | kernel_flags)
     ref = oracle.render(p, 256, 256, 64, flags=frm.FRM_FLAG_SCENE_SPHERE)
     assert np.array_equal(img, ref["rgba"])
     assert counters_of(st) == [int(c) for c in ref["counters"]]
 
 
-def test_ragged_sizes_and_edge_params(gpu_renderer_factory, oracle):
+@pytest.mark.parametrize("kernel_flags", [frm.FRM_FLAG_PERSISTENT_KERNEL, 0], ids=["persistent", "auto"])
+def test_ragged_sizes_and_edge_params(gpu_renderer_factory, oracle, kernel_flags):
     cases = [(1, 1, 18, 12), (7, 5, 0, 4), (33, 17, 15, 5), (130, 9, 16, 3), (9, 130, 18, 8)]
     for w, h, scene, iters in cases:
         p = params_for(scene, iters, 3.2175055, w, h)
-        img, st = gpu_render(gpu_renderer_factory, p, w, h, 200)
+        img, st = gpu_render(gpu_renderer_factory, p, w, h, 200, kernel_flags)
         ref = oracle.render(p, w, h, 200)
         assert np.array_equal(img, ref["rgba"]), (w, h, scene)
     # out-of-range scene index -> scene 0 (`case 0, default`); huge Sierpinski N wraps
     for scene, iters in ((19, 3), (1000, 2), (15, 33), (15, 31)):
         p = params_for(scene, iters, 0.5, 40, 24)
-        img, _ = gpu_render(gpu_renderer_factory, p, 40, 24, 100)
+        img, _ = gpu_render(gpu_renderer_factory, p, 40, 24, 100, kernel_flags)
         ref = oracle.render(p, 40, 24, 100)
         assert np.array_equal(img, ref["rgba"]), (scene, iters)
 
@@ -77,7 +79,7 @@ def test_camera_inside_geometry(gpu_renderer_factory, oracle):
     p2 = params_for(0, 3, 0.0, 64, 36)
     p2.update_camera(frm.Camera((0.1, 0.1, 0.1), 0.3, -0.2))
     for q in (p, p2):
-        img, _ = gpu_render(gpu_renderer_factory, q, 64, 36, 64)
+        img, _ = gpu_render(gpu_renderer_factory, q, 64, 36, 64, frm.FRM_FLAG_PERSISTENT_KERNEL)
         ref = oracle.render(q, 64, 36, 64)
         assert np.array_equal(img, ref["rgba"])
 
@@ -89,10 +91,27 @@ def test_scheduling_history_does_not_change_bytes(gpu_renderer_factory, oracle):
     q = params_for(18, 8, 1.0, 200, 120, pose="P2")
     ref_p = oracle.render(p, 200, 120, 256)
     ref_q = oracle.render(q, 200, 120, 256)
-    with gpu_renderer_factory(max_steps=256) as r:
+    with gpu_renderer_factory(max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL) as r:
         r.resize(200, 120)
         for params, ref in ((p, ref_p), (p, ref_p), (q, ref_q), (q, ref_q), (p, ref_p)):
             r.update_parameters_buffer(params)
             st = r.render()
             assert np.array_equal(r.read_frame(), ref["rgba"])
             assert counters_of(st) == [int(c) for c in ref["counters"]]
+
+
+def test_kernel_choice(gpu_renderer_factory):
+    """Without a kernel flag a launch below one resident persistent grid of pixels runs the
+    simple kernel (frm_kernel_for_pixels); the flags force either; both flags or an unknown
+    flag are refused at create."""
+    with gpu_renderer_factory() as r:
+        assert r.kernel_for(256 * 256) == "simple"
+        assert r.kernel_for(1920 * 1080) == "persistent"
+        assert r.kernel_for(3840 * 2160) == "persistent"
+    with gpu_renderer_factory(flags=frm.FRM_FLAG_SIMPLE_KERNEL) as r:
+        assert r.kernel_for(3840 * 2160) == "simple"
+    with gpu_renderer_factory(flags=frm.FRM_FLAG_PERSISTENT_KERNEL) as r:
+        assert r.kernel_for(1) == "persistent"
+    for bad in (frm.FRM_FLAG_SIMPLE_KERNEL | frm.FRM_FLAG_PERSISTENT_KERNEL, 0x80):
+        with pytest.raises(frm.FrmError):
+            gpu_renderer_factory(flags=bad)

@@ -32,7 +32,7 @@ def edit(path, old, new):
     path.write_text(s.replace(old, new))
 
 
-@pytest.mark.parametrize("kernel_flags", [0, frm.FRM_FLAG_SIMPLE_KERNEL], ids=["persistent", "simple"])
+@pytest.mark.parametrize("kernel_flags", [frm.FRM_FLAG_PERSISTENT_KERNEL, frm.FRM_FLAG_SIMPLE_KERNEL], ids=["persistent", "simple"])
 def test_reload_unmodified_sources_is_bit_exact(gpu_renderer_factory, oracle, tmp_path, kernel_flags):
     src = copy_sources(tmp_path, "csrc")
     with gpu_renderer_factory(max_steps=256, flags=kernel_flags) as r:
