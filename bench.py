@@ -70,32 +70,39 @@ def cpu_baseline(params, w, seconds):
     threads = max(1, min(threads, os.cpu_count() or 1))
     flags = 1 if w.sphere else 0
 
-    def sample(n):
+    def sample(n, nthreads):
         stride = max(1, w.height // max(1, n))
         rows = list(range(stride // 2, w.height, stride))
         t0 = time.perf_counter()
-        r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows, threads=threads)
+        r = frm_oracle.render(params, w.width, w.height, w.max_steps, flags=flags, rows=rows, threads=nthreads)
         return rows, stride, r, time.perf_counter() - t0
 
-    # calibrate with >= 2 rows per thread (fewer rows than threads would time the slowest
-    # row, not the pool), then size the sample to the target, twice at most
-    n = min(w.height, 2 * threads)
-    rows, stride, r, dt = sample(n)
-    for _ in range(2):
-        if dt >= 0.6 * seconds or len(rows) >= w.height:
-            break
-        n = min(w.height, int(len(rows) * seconds / max(dt, 1e-3)))
-        rows, stride, r, dt = sample(n)
-    c = r["counters"]
-    steps = int(c[2]) + int(c[3])
+    def timed(nthreads, target):
+        # calibrate with >= 2 rows per thread (fewer rows than threads would time the slowest
+        # row, not the pool), then size the sample to the target, twice at most
+        n = min(w.height, 2 * nthreads)
+        rows, stride, r, dt = sample(n, nthreads)
+        for _ in range(2):
+            if dt >= 0.6 * target or len(rows) >= w.height:
+                break
+            n = min(w.height, int(len(rows) * target / max(dt, 1e-3)))
+            rows, stride, r, dt = sample(n, nthreads)
+        steps = int(r["counters"][2]) + int(r["counters"][3])
+        text = (f"{len(rows)} evenly spaced rows (one in {stride}) of the {w.width}x{w.height} frame, "
+                f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O2, {nthreads} thread"
+                f"{'s' if nthreads > 1 else ''}")
+        return steps / dt / 1e9, text, (len(rows) / w.height) / dt
+
+    value, text, fps = timed(threads, seconds)
+    value1, text1, _ = timed(1, seconds / 3)  # also a 1-core timing
     return {
-        "value": steps / dt / 1e9,
+        "value": value,
         "unit": "Gray-march-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{len(rows)} evenly spaced rows (one in {stride}) of the {w.width}x{w.height} frame, "
-                  f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O2, {threads} threads",
-        "frames_per_s_extrapolated": (len(rows) / w.height) / dt,
+        "sample": text,
+        "frames_per_s_extrapolated": fps,
+        "single_core": {"value": value1, "unit": "Gray-march-steps/s", "cores": 1, "sample": text1},
     }
 
 
@@ -253,6 +260,7 @@ def main():
                                 if world > 1 else "single GPU"),
             },
             "frames_per_sec": args.steps * (world if split == 1 else 1) / elapsed,
+            "normal_de_evals_per_sec": st["normal_evals"] / elapsed,  # the 4 taps per hit, apart from steps
             "march_steps_per_frame": steps_total / args.steps / (world if split == 1 else 1),
             "roofline": {
                 "bound": "valu",
