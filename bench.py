@@ -6,13 +6,16 @@ iterations, 256 march steps, fixed camera pose P1; one "step" = one whole frame 
 hot path (fragment_main for every pixel) with inputs resident on the GPU.
 
 N GPUs (one process each, torch.distributed.run):
-* --split frames (default): alternate-frame rendering. Frames are independent units, so
-  each rank renders whole frames of the same workload, seen from the base pose rotated
-  about +y by rank * pi/4 (an orbit fly-through; rank 0 = the base pose). There is no
-  data-path collective and per-GPU work is fixed, so scaling is "weak".
-* --split rows: one frame split into interleaved row bands across the ranks, gathered to
-  rank 0 over RCCL and reassembled there (frm_unshuffle_bands): strong scaling, limited
-  by the longest pixel's sequential march.
+* --split rows (default): every frame is split into interleaved row bands across the
+  ranks, gathered to rank 0 over RCCL (xGMI) and reassembled there (frm_unshuffle_bands):
+  strong scaling of the fixed-pose workload, as BASELINE.json's north star describes. A
+  rank's share of a frame is short next to the frame's longest pixel (a sequential march),
+  so each rank keeps --inflight frames in flight (3 by default when split): frame k+1's
+  bands render while frame k's slowest pixels finish and frame k-1 is gathered.
+* --split frames: alternate-frame rendering. Frames are independent units, so each rank
+  renders whole frames of the same workload, seen from the base pose rotated about +y by
+  rank * pi/4 (an orbit fly-through; rank 0 = the base pose). There is no data-path
+  collective and per-GPU work is fixed, so scaling is "weak".
 
 Prints ONE JSON line on rank 0. `value` = G ray-march-steps/s of the whole job
 (primary + shadow march() iterations, counted exactly by the kernel, / wall time).
@@ -26,6 +29,15 @@ import json
 import os
 import sys
 import time
+
+# Frames in flight overlap only on distinct hardware queues. HIP maps streams onto at most
+# GPU_MAX_HW_QUEUES queues per process (4, HIP's default, which the GPU boxes export), shared
+# by the null stream, torch's streams, libfrm's and RCCL's; a render stream that shares a
+# queue with another waits behind its packets (measured: with 4 queues the second render
+# stream lands on the timing stream's queue and two frames in flight never overlap). Raised
+# before torch initialises HIP.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "fractal-ray-marching_amd")
@@ -49,10 +61,14 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "persistent", "simple"],
                     help="auto: libfrm's choice (simple below one resident persistent grid of pixels)")
     ap.add_argument("--band-rows", type=int, default=0)
-    ap.add_argument("--split", default="frames", choices=["frames", "rows"],
-                    help="N>1: 'frames' = alternate-frame rendering, each rank renders whole frames of "
-                    "an orbit fly-through (no data-path collective, weak scaling); 'rows' = one frame "
-                    "split into interleaved row bands + RCCL gather to rank 0 (strong scaling)")
+    ap.add_argument("--split", default="rows", choices=["frames", "rows"],
+                    help="N>1: 'rows' = every frame split into interleaved row bands + RCCL gather to "
+                    "rank 0 (strong scaling); 'frames' = alternate-frame rendering, each rank renders "
+                    "whole frames of an orbit fly-through (no data-path collective, weak scaling)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight per GPU (frm_config.frames_in_flight): frame k+1 renders "
+                    "while frame k's longest pixels finish; 1 = one frame at a time; 0 = 2 for whole "
+                    "frames, 3 for a rank's bands of a split frame (measured best, DESIGN.md)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
@@ -158,40 +174,46 @@ def main():
         params.update_camera(cam)
     flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
         {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel])
-    r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags)
+    split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
+    inflight = args.inflight or (2 if split == 1 else 3)
+    inflight = max(1, min(inflight, frm.FRM_MAX_FRAMES_IN_FLIGHT))
+    r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=inflight)
     r.resize(w.width, w.height)
     r.update_parameters_buffer(params)
     if args.reload:
         r.reload(args.reload)
 
-    split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
     band_rows = args.band_rows or (w.height if split == 1 else tiling.choose_band_rows(w.height, world))
     local_pixels = w.width * min(w.height, tiling.rank_rows(w.height, band_rows, 0 if split == 1 else rank, split))
     kernel_used = r.kernel_for(local_pixels) + (" (auto)" if args.kernel == "auto" else "")
     dev = torch.device("cuda", local)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
-    # A dedicated stream: its handle is non-null, so libfrm launches on it (a NULL handle
-    # means "the context's own stream") and the HIP events below bracket the kernels.
-    stream = torch.cuda.Stream(device=dev)
-    torch.cuda.set_stream(stream)
+    # Frame k renders (and, split over ranks, is gathered and unshuffled) on streams[k % F]:
+    # dedicated streams, so their handles are non-null and libfrm launches on them (a NULL
+    # handle means "the context's own stream"), and the HIP events below see the kernels.
+    streams = [torch.cuda.Stream(device=dev) for _ in range(inflight)]
+    main_stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(main_stream)
     kev = []  # (start, stop) HIP events around every render launch of the timed region
     timing = {"on": False}
 
-    def render_bands(buf, br, first, stride):
+    def render_bands(buf, br, first, stride, slot):
+        s = streams[slot]
         ev = None
         if timing["on"]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record(stream)
-        r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, stream.cuda_stream, counters.data_ptr())
+            ev[0].record(s)
+        r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
         if ev is not None:
-            ev[1].record(stream)
+            ev[1].record(s)
             kev.append(ev)
 
-    def unshuffle(gathered, frame):
+    def unshuffle(gathered, frame, slot):
         r.unshuffle_bands(gathered.data_ptr(), gathered.numel() // world, frame.data_ptr(), frame.numel(),
-                          band_rows, world, stream.cuda_stream)
+                          band_rows, world, streams[slot].cuda_stream)
 
-    tf = RowTiledFrame(w.width, w.height, 0 if split == 1 else rank, split, band_rows, dev, render_bands, unshuffle)
+    tf = RowTiledFrame(w.width, w.height, 0 if split == 1 else rank, split, band_rows, dev, render_bands, unshuffle,
+                       inflight=inflight, streams=streams)
 
     # Animated workloads (C5): every frame advances time by 1/60 s through the reference's
     # Timing::update (frm_timing_update), as the reference's frame loop does
@@ -213,16 +235,28 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timing["on"] = True
+    # device span of the timed region on the render streams: every stream waits for `begin`,
+    # `end` waits for every stream
+    begin, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    begin.record(main_stream)
+    for s in streams:
+        s.wait_event(begin)
     t0 = time.perf_counter()
     tf.run(args.steps, before_frame)
+    for s in streams:
+        e = torch.cuda.Event()
+        e.record(s)
+        main_stream.wait_event(e)
+    end.record(main_stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in kev)
+    span_ms = begin.elapsed_time(end)
+    launch_ms = sum(a.elapsed_time(b) for a, b in kev) / max(1, len(kev))
 
-    stats_vec = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    stats_vec = torch.tensor([elapsed, span_ms], dtype=torch.float64, device=dev)
     cnt = counters.clone()
     if world > 1:
         dist.all_reduce(stats_vec[:1], op=dist.ReduceOp.MAX)
@@ -232,7 +266,10 @@ def main():
     st = r.stats_from_counters(c)
     steps_total = st["march_steps"]
     if rank == 0:
-        avg_kernel_s = kernel_ms / 1e3 / args.steps
+        # per-frame device time of the pipelined render (the HIP-event span of the timed
+        # region / frames): with F frames in flight launches overlap, so a single launch's
+        # start-to-end time (avg_launch_ms) also holds the previous frame's tail
+        avg_kernel_s = span_ms / 1e3 / args.steps
         wom_per_launch = st["wom_ops"] / args.steps / world
         achieved = wom_per_launch / avg_kernel_s / 1e12
         traffic, traffic_src = pmc_traffic(args.workload, world)
@@ -252,7 +289,7 @@ def main():
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
-                "pose": args.pose, "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
+                "pose": args.pose, "frames_in_flight": inflight, "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if split > 1 else
                                 f"alternate-frame rendering x{world}: rank r renders the {args.pose} view "
@@ -272,6 +309,8 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": "frm::render",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
+                "avg_launch_ms": launch_ms,
+                "timing": "HIP events on the render streams: span of the timed region / frames",
                 "algorithmic_ops_per_launch": wom_per_launch,
                 "model": "WOM VALU lane-ops counted from fragment.wgsl (DESIGN.md §Roofline)",
             },

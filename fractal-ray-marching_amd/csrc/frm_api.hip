@@ -27,24 +27,20 @@ static constexpr uint32_t kDefaultServiceMin = 20;  // swept 16..36 on MI355X (r
 // its load balancing: 256x256 runs 23 G steps/s simple vs 10 persistent, 1920x1080 8 vs 20.
 static constexpr uint64_t kSimplePixelsPerCu = 1536;
 
-struct frm_ctx {
-  int device = 0;
-  uint32_t max_steps = FRM_DEFAULT_MAX_STEPS;
-  uint32_t flags = 0;
-  int cu_count = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-  uint32_t width = 0, height = 0;
-  uint8_t* fb = nullptr;
-  ReloadedKernels* reloaded = nullptr;  // frm_reload: kernels compiled from edited sources
-  uint8_t* present_buf = nullptr;  // frm_present output, grown on demand
-  size_t present_cap = 0;
-  unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
+// One frame in flight: the device state a render launch owns until it completes. A context
+// has config.frames_in_flight slots and launches round-robin over them, so frame k+1 can
+// start (its own scratch, queue and framebuffer) while frame k's last pixels finish.
+struct Slot {
+  hipStream_t stream = nullptr;  // frm_render's stream for this slot (slot 0: the context stream)
+  hipEvent_t done = nullptr;     // recorded after the slot's last launch (any stream)
+  bool pending = false;          // `done` has been recorded since the slot was last waited for
+  hipStream_t last_stream = nullptr;  // stream of the slot's last launch
+  uint8_t* fb = nullptr;         // frm_render's framebuffer for this slot
   unsigned int* queue = nullptr;
   ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
   size_t records_cap = 0;
   // pixel scheduling state (frm_sched.hip), sched_cap entries each: 0..cap-1, the fetch
-  // order, the cost keys the last launch recorded per pixel and the sort's key output
+  // order, the cost keys the slot's last launch recorded per pixel and the sort's key output
   uint32_t* sched_iota = nullptr;
   uint32_t* sched_order = nullptr;
   uint8_t* sched_keys = nullptr;  // 2 x sched_cap: keys, sorted keys
@@ -52,6 +48,24 @@ struct frm_ctx {
   size_t sched_cap = 0, sched_temp_bytes = 0;
   uint64_t sched_key = 0;  // geometry the recorded keys belong to
   bool sched_history = false;
+};
+
+struct frm_ctx {
+  int device = 0;
+  uint32_t max_steps = FRM_DEFAULT_MAX_STEPS;
+  uint32_t flags = 0;
+  int cu_count = 0;
+  hipStream_t stream = nullptr;  // the context stream (= slots[0].stream)
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  uint32_t width = 0, height = 0;
+  Slot slots[FRM_MAX_FRAMES_IN_FLIGHT];
+  uint32_t nslots = 1;
+  uint32_t next_slot = 0;  // slot of the next launch
+  uint32_t last_slot = 0;  // slot of the last frm_render (the frame read_frame/present see)
+  ReloadedKernels* reloaded = nullptr;  // frm_reload: kernels compiled from edited sources
+  uint8_t* present_buf = nullptr;  // frm_present output, grown on demand
+  size_t present_cap = 0;
+  unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   uint32_t service_min = kDefaultServiceMin;
   frm_parameters params{};
   bool has_params = false;
@@ -107,7 +121,7 @@ uint32_t band_valid_rows(uint32_t height, const BandGeometry& g) {
 
 int ensure_ready(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
-  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
   if (!ctx->has_params) return fail(ctx, FRM_ERR_NOT_READY, "frm_set_parameters has not been called");
   return FRM_OK;
 }
@@ -124,7 +138,6 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.g.local_rows = local_rows;
   a.out = (uint32_t*)dst;
   a.counters = counters;
-  a.queue = ctx->queue;
   a.npix = band_valid_rows(ctx->height, a.g) * ctx->width;
   a.service_min = ctx->service_min;
   return a;
@@ -136,59 +149,101 @@ KernelKind kernel_for(const frm_ctx* ctx, uint64_t pixels) {
   return pixels < kSimplePixelsPerCu * (uint64_t)ctx->cu_count ? kKernelSimple : kKernelPersistent;
 }
 
-int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s) {
+// Waits (host) until the slot's last launch has completed.
+int wait_slot(frm_ctx* ctx, Slot& sl) {
+  if (sl.pending) {
+    FRM_HIP(ctx, hipEventSynchronize(sl.done));
+    sl.pending = false;
+  }
+  return FRM_OK;
+}
+
+int synchronize_all(frm_ctx* ctx) {
+  for (uint32_t i = 0; i < ctx->nslots; ++i) {
+    Slot& sl = ctx->slots[i];
+    if (sl.stream) FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
+    int rc = wait_slot(ctx, sl);
+    if (rc) return rc;
+  }
+  return FRM_OK;
+}
+
+// The stream frm_render uses for slot i (created on first use: a context with one frame in
+// flight never creates more than the context stream).
+int slot_stream(frm_ctx* ctx, uint32_t i, hipStream_t* out) {
+  Slot& sl = ctx->slots[i];
+  if (!sl.stream) FRM_HIP(ctx, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+  *out = sl.stream;
+  return FRM_OK;
+}
+
+// Enqueues one render launch on stream s with the scratch of the context's next slot.
+// Stream order covers a slot reused on the same stream; a slot last used on another
+// stream is awaited on the device (hipStreamWaitEvent), so callers may rotate streams.
+int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullptr) {
   if (a.g.local_rows == 0) return FRM_OK;
+  const uint32_t si = ctx->next_slot;
+  Slot& sl = ctx->slots[si];
+  if (sl.pending && sl.last_stream != s) FRM_HIP(ctx, hipStreamWaitEvent(s, sl.done, 0));
   const KernelKind kind = kernel_for(ctx, a.npix);
+  a.queue = sl.queue;
   if (kind == kKernelPersistent) {
     const size_t need = (size_t)a.g.local_rows * a.f.width;
-    if (need > ctx->records_cap) {  // grows outside the steady state (first frame of a size)
-      FRM_HIP(ctx, hipStreamSynchronize(s));
-      if (ctx->records) FRM_HIP(ctx, hipFree(ctx->records));
-      ctx->records = nullptr;
-      ctx->records_cap = 0;
-      FRM_HIP(ctx, hipMalloc(&ctx->records, need * sizeof(ShadeRecord)));
-      ctx->records_cap = need;
+    if (need > sl.records_cap) {  // grows outside the steady state (first frame of a size)
+      int rc = wait_slot(ctx, sl);
+      if (rc) return rc;
+      if (sl.records) FRM_HIP(ctx, hipFree(sl.records));
+      sl.records = nullptr;
+      sl.records_cap = 0;
+      FRM_HIP(ctx, hipMalloc(&sl.records, need * sizeof(ShadeRecord)));
+      sl.records_cap = need;
     }
-    a.records = ctx->records;
-    // pixel scheduling: fetch this launch's pixels by the cost recorded last time for the
-    // same geometry (most expensive first)
+    a.records = sl.records;
+    // pixel scheduling: fetch this launch's pixels by the cost the slot recorded last time
+    // for the same geometry (most expensive first)
     const uint32_t npix = a.npix;
-    if (npix > ctx->sched_cap) {
-      FRM_HIP(ctx, hipStreamSynchronize(s));
-      for (void* b : {(void*)ctx->sched_iota, (void*)ctx->sched_order, (void*)ctx->sched_keys, ctx->sched_temp})
+    if (npix > sl.sched_cap) {
+      int rc = wait_slot(ctx, sl);
+      if (rc) return rc;
+      for (void* b : {(void*)sl.sched_iota, (void*)sl.sched_order, (void*)sl.sched_keys, sl.sched_temp})
         if (b) FRM_HIP(ctx, hipFree(b));
-      ctx->sched_iota = ctx->sched_order = nullptr;
-      ctx->sched_keys = nullptr;
-      ctx->sched_temp = nullptr;
-      ctx->sched_cap = 0;
-      ctx->sched_temp_bytes = schedule_temp_bytes(npix);
-      FRM_HIP(ctx, hipMalloc(&ctx->sched_iota, (size_t)npix * sizeof(uint32_t)));
-      FRM_HIP(ctx, hipMalloc(&ctx->sched_order, (size_t)npix * sizeof(uint32_t)));
-      FRM_HIP(ctx, hipMalloc(&ctx->sched_keys, (size_t)npix * 2));
-      FRM_HIP(ctx, hipMalloc(&ctx->sched_temp, ctx->sched_temp_bytes ? ctx->sched_temp_bytes : 16));
-      FRM_HIP(ctx, fill_iota(ctx->sched_iota, npix, s));
-      ctx->sched_cap = npix;
-      ctx->sched_history = false;
+      sl.sched_iota = sl.sched_order = nullptr;
+      sl.sched_keys = nullptr;
+      sl.sched_temp = nullptr;
+      sl.sched_cap = 0;
+      sl.sched_temp_bytes = schedule_temp_bytes(npix);
+      FRM_HIP(ctx, hipMalloc(&sl.sched_iota, (size_t)npix * sizeof(uint32_t)));
+      FRM_HIP(ctx, hipMalloc(&sl.sched_order, (size_t)npix * sizeof(uint32_t)));
+      FRM_HIP(ctx, hipMalloc(&sl.sched_keys, (size_t)npix * 2));
+      FRM_HIP(ctx, hipMalloc(&sl.sched_temp, sl.sched_temp_bytes ? sl.sched_temp_bytes : 16));
+      FRM_HIP(ctx, fill_iota(sl.sched_iota, npix, s));
+      sl.sched_cap = npix;
+      sl.sched_history = false;
     }
     const uint64_t key = ((uint64_t)a.f.width << 40) ^ ((uint64_t)a.g.local_rows << 20) ^
                          ((uint64_t)a.g.band_rows << 8) ^ ((uint64_t)a.g.first_band << 4) ^ a.g.band_stride ^
                          ((uint64_t)a.f.height << 52);
-    const bool history = ctx->sched_history && key == ctx->sched_key;
-    FRM_HIP(ctx, schedule_pixels(npix, history, ctx->sched_keys, ctx->sched_keys + ctx->sched_cap,
-                                 ctx->sched_iota, ctx->sched_order, ctx->sched_temp, ctx->sched_temp_bytes, s));
-    a.pixel_order = ctx->sched_order;
-    a.pixel_key = ctx->sched_keys;
-    ctx->sched_key = key;
-    ctx->sched_history = true;
-    a.debug = (unsigned long long*)(ctx->queue + 8);  // bytes 32..71 of the queue block
-    FRM_HIP(ctx, hipMemsetAsync(ctx->queue, 0, sizeof(unsigned int), s));
+    const bool history = sl.sched_history && key == sl.sched_key;
+    FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
+                                 sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
+    a.pixel_order = sl.sched_order;
+    a.pixel_key = sl.sched_keys;
+    sl.sched_key = key;
+    sl.sched_history = true;
+    a.debug = (unsigned long long*)(sl.queue + 8);  // bytes 32..71 of the queue block
+    FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, sizeof(unsigned int), s));
 #ifdef FRM_STAMPS
-    FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 8, 0, 16, s));
-    FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 12, 0xff, 16, s));  // atomicMin slots
-    FRM_HIP(ctx, hipMemsetAsync(ctx->queue + 16, 0, 8, s));
+    FRM_HIP(ctx, hipMemsetAsync(sl.queue + 8, 0, 16, s));
+    FRM_HIP(ctx, hipMemsetAsync(sl.queue + 12, 0xff, 16, s));  // atomicMin slots
+    FRM_HIP(ctx, hipMemsetAsync(sl.queue + 16, 0, 8, s));
 #endif
   }
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded));
+  FRM_HIP(ctx, hipEventRecord(sl.done, s));
+  sl.pending = true;
+  sl.last_stream = s;
+  ctx->next_slot = (si + 1u) % ctx->nslots;
+  if (out_slot) *out_slot = si;
   return FRM_OK;
 }
 
@@ -215,7 +270,9 @@ int frm_device_count(int32_t* out_count) {
 int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   if (!out_ctx || !config) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "out_ctx/config is NULL");
   *out_ctx = nullptr;
-  if (config->reserved != 0) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.reserved must be 0");
+  if (config->frames_in_flight > FRM_MAX_FRAMES_IN_FLIGHT)
+    return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.frames_in_flight %u above %u", config->frames_in_flight,
+                FRM_MAX_FRAMES_IN_FLIGHT);
   const uint32_t kernels = FRM_FLAG_SIMPLE_KERNEL | FRM_FLAG_PERSISTENT_KERNEL;
   if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE)) || (config->flags & kernels) == kernels)
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.flags 0x%x: unknown flag or both kernel flags",
@@ -231,6 +288,7 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   ctx->device = config->device;
   ctx->max_steps = config->max_steps ? config->max_steps : FRM_DEFAULT_MAX_STEPS;
   ctx->flags = config->flags;
+  ctx->nslots = config->frames_in_flight ? config->frames_in_flight : 1u;
   if (const char* env = getenv("FRM_SERVICE_MIN")) {
     long v = strtol(env, nullptr, 10);
     if (v >= 1 && v <= 64) ctx->service_min = (uint32_t)v;
@@ -245,7 +303,12 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
     if ((e = hipEventCreate(&ctx->ev_start)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
     if ((e = hipEventCreate(&ctx->ev_stop)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
     if ((e = hipMalloc(&ctx->counters, FRM_NUM_COUNTERS * sizeof(unsigned long long))) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(counters)"); break; }
-    if ((e = hipMalloc(&ctx->queue, 128)) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(queue)"); break; }
+    ctx->slots[0].stream = ctx->stream;
+    for (uint32_t i = 0; i < ctx->nslots && rc == FRM_OK; ++i) {
+      Slot& sl = ctx->slots[i];
+      if ((e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming)) != hipSuccess) rc = hip_fail(ctx, e, "hipEventCreate");
+      else if ((e = hipMalloc(&sl.queue, 128)) != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc(queue)");
+    }
   } while (0);
   if (rc != FRM_OK) {
     g_error = ctx->error;
@@ -260,16 +323,22 @@ int frm_destroy(frm_ctx* ctx) {
   if (!ctx) return FRM_OK;
   // Teardown is best effort: statuses are ignored so every resource gets released.
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->fb) (void)hipFree(ctx->fb);
+  for (uint32_t i = 0; i < ctx->nslots; ++i) {
+    Slot& sl = ctx->slots[i];
+    if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+    if (sl.pending) (void)hipEventSynchronize(sl.done);
+  }
+  for (uint32_t i = 0; i < ctx->nslots; ++i) {
+    Slot& sl = ctx->slots[i];
+    for (void* b : {(void*)sl.fb, (void*)sl.queue, (void*)sl.records, (void*)sl.sched_iota, (void*)sl.sched_order,
+                    (void*)sl.sched_keys, sl.sched_temp})
+      if (b) (void)hipFree(b);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    if (i > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
+  }
   if (ctx->present_buf) (void)hipFree(ctx->present_buf);
   unload_reloaded(ctx->reloaded);
   if (ctx->counters) (void)hipFree(ctx->counters);
-  if (ctx->queue) (void)hipFree(ctx->queue);
-  if (ctx->records) (void)hipFree(ctx->records);
-  for (void* b : {(void*)ctx->sched_iota, (void*)ctx->sched_order, (void*)ctx->sched_keys})
-    if (b) (void)hipFree(b);
-  if (ctx->sched_temp) (void)hipFree(ctx->sched_temp);
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -283,16 +352,19 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "frame size %ux%u outside [1, %u]^2", width, height,
                 FRM_MAX_DIMENSION);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
-  if (ctx->fb && width == ctx->width && height == ctx->height) return FRM_OK;
-  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if (ctx->fb) {
-    FRM_HIP(ctx, hipFree(ctx->fb));
-    ctx->fb = nullptr;
+  if (ctx->slots[0].fb && width == ctx->width && height == ctx->height) return FRM_OK;
+  int rc = synchronize_all(ctx);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < ctx->nslots; ++i) {  // slots > 0 allocate theirs at first use
+    Slot& sl = ctx->slots[i];
+    if (sl.fb) FRM_HIP(ctx, hipFree(sl.fb));
+    sl.fb = nullptr;
   }
   ctx->width = ctx->height = 0;
-  FRM_HIP(ctx, hipMalloc(&ctx->fb, (size_t)width * height * 4u));
+  FRM_HIP(ctx, hipMalloc(&ctx->slots[0].fb, (size_t)width * height * 4u));
   ctx->width = width;
   ctx->height = height;
+  ctx->last_slot = 0;
   return FRM_OK;
 }
 
@@ -311,18 +383,25 @@ int frm_render(frm_ctx* ctx, frm_stats* stats) {
   int rc = ensure_ready(ctx);
   if (rc) return rc;
   FRM_HIP(ctx, hipSetDevice(ctx->device));
-  KernelArgs a = make_args(ctx, ctx->fb, ctx->counters, ctx->height, 0, 1, ctx->height);
+  if (stats && (rc = synchronize_all(ctx))) return rc;  // the counters must hold this frame alone
+  const uint32_t si = ctx->next_slot;
+  Slot& sl = ctx->slots[si];
+  hipStream_t s;
+  if ((rc = slot_stream(ctx, si, &s))) return rc;
+  if (!sl.fb) FRM_HIP(ctx, hipMalloc(&sl.fb, (size_t)ctx->width * ctx->height * 4u));
+  KernelArgs a = make_args(ctx, sl.fb, ctx->counters, ctx->height, 0, 1, ctx->height);
   if (stats) {
-    FRM_HIP(ctx, hipMemsetAsync(ctx->counters, 0, FRM_NUM_COUNTERS * sizeof(unsigned long long), ctx->stream));
-    FRM_HIP(ctx, hipEventRecord(ctx->ev_start, ctx->stream));
+    FRM_HIP(ctx, hipMemsetAsync(ctx->counters, 0, FRM_NUM_COUNTERS * sizeof(unsigned long long), s));
+    FRM_HIP(ctx, hipEventRecord(ctx->ev_start, s));
   }
-  rc = launch(ctx, a, ctx->stream);
+  rc = launch(ctx, a, s);
   if (rc) return rc;
+  ctx->last_slot = si;
   if (stats) {
-    FRM_HIP(ctx, hipEventRecord(ctx->ev_stop, ctx->stream));
+    FRM_HIP(ctx, hipEventRecord(ctx->ev_stop, s));
     uint64_t host[FRM_NUM_COUNTERS];
-    FRM_HIP(ctx, hipMemcpyAsync(host, ctx->counters, sizeof(host), hipMemcpyDeviceToHost, ctx->stream));
-    FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    FRM_HIP(ctx, hipMemcpyAsync(host, ctx->counters, sizeof(host), hipMemcpyDeviceToHost, s));
+    FRM_HIP(ctx, hipStreamSynchronize(s));
     float ms = 0.0f;
     FRM_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
     rc = frm_stats_from_counters(ctx, host, stats);
@@ -334,20 +413,21 @@ int frm_render(frm_ctx* ctx, frm_stats* stats) {
 
 int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes) {
   if (!ctx || !dst) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/dst is NULL");
-  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
   size_t need = (size_t)ctx->width * ctx->height * 4u;
   if (dst_bytes < need)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, frame needs %zu", dst_bytes, need);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
-  FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->fb, need, hipMemcpyDeviceToHost, ctx->stream));
-  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
+  FRM_HIP(ctx, hipMemcpyAsync(dst, sl.fb, need, hipMemcpyDeviceToHost, sl.stream));
+  FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
   return FRM_OK;
 }
 
 int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags, uint8_t* dst,
                 size_t dst_bytes) {
   if (!ctx || !dst) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/dst is NULL");
-  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
   if (out_width == 0 || out_height == 0 || out_width > FRM_MAX_DIMENSION || out_height > FRM_MAX_DIMENSION)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad output size %ux%u", out_width, out_height);
   if (flags & ~(FRM_BLIT_SRGB | FRM_BLIT_BGRA)) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
@@ -355,18 +435,19 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
   if (dst_bytes < need)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, output needs %zu", dst_bytes, need);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  const Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
   if (need > ctx->present_cap) {
-    FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
     if (ctx->present_buf) FRM_HIP(ctx, hipFree(ctx->present_buf));
     ctx->present_buf = nullptr;
     ctx->present_cap = 0;
     FRM_HIP(ctx, hipMalloc(&ctx->present_buf, need));
     ctx->present_cap = need;
   }
-  FRM_HIP(ctx, launch_blit(ctx->fb, ctx->width, ctx->height, ctx->present_buf, out_width, out_height, flags,
-                           ctx->stream));
-  FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->present_buf, need, hipMemcpyDeviceToHost, ctx->stream));
-  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  FRM_HIP(ctx, launch_blit(sl.fb, ctx->width, ctx->height, ctx->present_buf, out_width, out_height, flags,
+                           sl.stream));
+  FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->present_buf, need, hipMemcpyDeviceToHost, sl.stream));
+  FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
   return FRM_OK;
 }
 
@@ -389,8 +470,7 @@ int frm_reload(frm_ctx* ctx, const char* source_dir) {
 int frm_synchronize(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
   FRM_HIP(ctx, hipSetDevice(ctx->device));
-  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return FRM_OK;
+  return synchronize_all(ctx);
 }
 
 int frm_kernel_for_pixels(const frm_ctx* ctx, uint64_t pixels, uint32_t* out_kernel) {
@@ -428,7 +508,7 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
                         size_t dst_bytes, uint32_t band_rows, uint32_t ranks, void* stream) {
   if (!ctx || !dev_src || !dev_dst || band_rows == 0 || ranks == 0)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "invalid unshuffle arguments");
-  if (!ctx->fb) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
   size_t need = (size_t)ctx->width * ctx->height * 4u;
   if (dst_bytes < need)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, frame needs %zu", dst_bytes, need);
@@ -446,13 +526,15 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
 
 #ifdef FRM_STAMPS
 extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
-  return hipMemcpy(out5, ctx->queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+  const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
+  return hipMemcpy(out5, sl.queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 // per-pixel cost keys recorded by the last persistent launch (local pixel order; before
 // the next launch overwrites them)
 extern "C" int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
-  if (n > ctx->sched_cap) n = ctx->sched_cap;
-  return hipMemcpy(out, ctx->sched_keys, n, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+  const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
+  if (n > sl.sched_cap) n = sl.sched_cap;
+  return hipMemcpy(out, sl.sched_keys, n, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 #endif
 

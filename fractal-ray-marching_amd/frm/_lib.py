@@ -22,6 +22,7 @@ FRM_ERR_UNSUPPORTED = 7
 FRM_ERR_COMPILE = 8
 
 FRM_NUM_SCENES = 19
+FRM_MAX_FRAMES_IN_FLIGHT = 4
 FRM_DEFAULT_MAX_STEPS = 5000
 FRM_MAX_NUM_ITERATIONS = 4096
 FRM_NUM_COUNTERS = 8
@@ -52,7 +53,7 @@ class FrmConfig(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("max_steps", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("frames_in_flight", ctypes.c_uint32),
     ]
 
 

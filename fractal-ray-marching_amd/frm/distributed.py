@@ -2,11 +2,15 @@
 interleaved row bands r, r+P, r+2P, ... of every frame into a local buffer, the buffers
 are gathered to rank 0 with torch.distributed (RCCL over xGMI on MI355X, gloo in the CPU
 tests) and rank 0 reassembles the frame. Frame k's gather overlaps frame k+1's render:
-two local buffers and two gather targets alternate, and rank 0 unshuffles frame k only
-after issuing frame k+1's render.
+local buffers and gather targets alternate, and rank 0 unshuffles frame k only after
+issuing frame k+1's render. With `inflight` F > 1, frames rotate over F streams and
+F buffer sets, so frame k+1's render also overlaps frame k's: a rank's share of one
+frame is short next to its longest pixel's sequential march.
 
 The band renderer and the unshuffle are injected (libfrm on the GPU, the oracle/numpy in
 tests) so the scheduling logic here is exactly what bench.py runs."""
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -15,43 +19,66 @@ from . import tiling
 
 class RowTiledFrame:
     def __init__(self, width, height, rank, world, band_rows, device, render_bands, unshuffle,
-                 group=None):
-        """render_bands(buf, band_rows, first_band, band_stride): enqueue the render of this
-        rank's bands into the uint8 tensor buf (device memory for the GPU path).
-        unshuffle(gathered, frame): rank 0 only; rank-major band buffers -> row-major frame."""
+                 group=None, inflight=1, streams=None):
+        """render_bands(buf, band_rows, first_band, band_stride, slot): enqueue the render of
+        this rank's bands into the uint8 tensor buf (device memory for the GPU path) for
+        frame slot `slot` (k % inflight; the GPU path renders it on streams[slot]).
+        unshuffle(gathered, frame, slot): rank 0 only; rank-major band buffers -> row-major
+        frame. inflight = frames in flight: frame k's render, gather and unshuffle are
+        enqueued on streams[k % inflight] (torch streams; None = the current stream, as in
+        the CPU tests), so up to `inflight` frames overlap on the GPU."""
         self.width, self.height = width, height
         self.rank, self.world = rank, world
         self.band_rows = band_rows
         self.render_bands = render_bands
         self.unshuffle = unshuffle
         self.group = group
+        self.inflight = max(1, inflight)
+        self.streams = streams
+        if streams is not None and len(streams) != self.inflight:
+            raise ValueError(f"{len(streams)} streams for {self.inflight} frames in flight")
         self.rows_local = tiling.rank_buffer_rows(height, band_rows, world)
         self.nbytes = self.rows_local * width * 4
-        nbuf = 2 if world > 1 else 1
+        # buffer k % nbuf serves frame k. Reuse is safe in stream order: frame k + nbuf runs
+        # on frame k's stream (nbuf is a multiple of inflight), after frame k's gather wait
+        # and unshuffle, which _finish(k) enqueues before frame k + nbuf is issued.
+        nbuf = self.inflight if self.inflight > 1 else (2 if world > 1 else 1)
+        self.nbuf = nbuf
         self.bufs = [torch.zeros(self.nbytes, dtype=torch.uint8, device=device) for _ in range(nbuf)]
-        self.gathered = self.frame = None
+        self.gathered = self.frames = None
         if world > 1 and rank == 0:
             self.gathered = [torch.zeros(world * self.nbytes, dtype=torch.uint8, device=device)
-                             for _ in range(2)]
-            self.frame = torch.zeros(height * width * 4, dtype=torch.uint8, device=device)
+                             for _ in range(nbuf)]
+            self.frames = [torch.zeros(height * width * 4, dtype=torch.uint8, device=device)
+                           for _ in range(nbuf)]
         self.frames_done = 0
+        self.last = 0
+
+    def _stream(self, k):
+        if self.streams is None:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.streams[k % self.inflight])
 
     def _issue(self, k):
-        buf = self.bufs[k % len(self.bufs)]
-        self.render_bands(buf, self.band_rows, self.rank, self.world)
-        if self.world == 1:
-            return None
-        glist = None
-        if self.rank == 0:
-            g = self.gathered[k % 2]
-            glist = [g[i * self.nbytes:(i + 1) * self.nbytes] for i in range(self.world)]
-        return dist.gather(buf, gather_list=glist, dst=0, group=self.group, async_op=True)
+        buf = self.bufs[k % self.nbuf]
+        with self._stream(k):
+            self.render_bands(buf, self.band_rows, self.rank, self.world, k % self.inflight)
+            if self.world == 1:
+                return None
+            glist = None
+            if self.rank == 0:
+                g = self.gathered[k % self.nbuf]
+                glist = [g[i * self.nbytes:(i + 1) * self.nbytes] for i in range(self.world)]
+            return dist.gather(buf, gather_list=glist, dst=0, group=self.group, async_op=True)
 
     def _finish(self, k, work):
         if work is not None:
-            work.wait()
-            if self.rank == 0:
-                self.unshuffle(self.gathered[k % 2], self.frame)
+            with self._stream(k):
+                work.wait()  # NCCL: the stream waits for the gather (the host does not)
+                if self.rank == 0:
+                    self.unshuffle(self.gathered[k % self.nbuf], self.frames[k % self.nbuf],
+                                   k % self.inflight)
+        self.last = k % self.nbuf
         self.frames_done += 1
 
     def run(self, n, before_frame=None):
@@ -72,5 +99,5 @@ class RowTiledFrame:
     def output(self):
         """Rank 0: the last frame, flat RGBA8 (the band buffer itself when world == 1)."""
         if self.world == 1:
-            return self.bufs[0]
-        return self.frame
+            return self.bufs[self.last]
+        return self.frames[self.last]

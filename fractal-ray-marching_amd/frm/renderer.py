@@ -11,13 +11,14 @@ from . import _lib
 
 
 class Renderer:
-    def __init__(self, device=0, max_steps=0, flags=0):
+    def __init__(self, device=0, max_steps=0, flags=0, frames_in_flight=1):
         lib = _lib.load()
         self._lib = lib
         self.ctx = ctypes.c_void_p()
-        cfg = _lib.FrmConfig(device, max_steps, flags, 0)
+        cfg = _lib.FrmConfig(device, max_steps, flags, frames_in_flight)
         _lib.check(lib.frm_create(ctypes.byref(self.ctx), ctypes.byref(cfg)))
         self.device = device
+        self.frames_in_flight = max(1, frames_in_flight)
         self.width = self.height = 0
 
     def close(self):

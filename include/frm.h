@@ -16,7 +16,9 @@
  *   - A context drives one GPU and is not thread-safe (one context per host thread),
  *     mirroring the reference's single winit event-loop thread (src/app.rs).
  *   - Rendering is stream-ordered. frm_render() with a NULL stats pointer is
- *     asynchronous; frm_read_frame()/frm_synchronize() wait for it.
+ *     asynchronous; frm_read_frame()/frm_synchronize() wait for it. With
+ *     frames_in_flight > 1, consecutive frm_render() calls run on rotating streams and
+ *     may overlap on the GPU; frm_read_frame()/frm_present() see the last one.
  *   - Plain pointers and sizes only; `void* stream` is a hipStream_t (NULL = the
  *     context's own stream).
  */
@@ -32,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FRM_ABI_VERSION 1u
+#define FRM_ABI_VERSION 2u  /* 2: frm_config.frames_in_flight (was reserved) */
 
 /* ---- status codes -------------------------------------------------------- */
 enum {
@@ -101,8 +103,16 @@ typedef struct frm_config {
   uint32_t max_steps; /* march() step cap; 0 = FRM_DEFAULT_MAX_STEPS. It also feeds the
                          ambient-occlusion term (fragment.wgsl:289,342)               */
   uint32_t flags;     /* FRM_FLAG_*                                                    */
-  uint32_t reserved;  /* must be 0                                                     */
+  uint32_t frames_in_flight; /* frames a context may have in flight on the GPU at once,
+                         1..FRM_MAX_FRAMES_IN_FLIGHT (0 = 1). Each render launch (frm_render,
+                         frm_render_bands) takes the next of this many slots of device scratch
+                         (pixel records, scheduling arrays, work queue; frm_render: also a
+                         framebuffer and a stream), so frame k+1 runs while frame k's longest
+                         pixels finish instead of after them. No reference counterpart: the
+                         reference renders one frame per submit (graphics.rs:91-110).        */
 } frm_config;
+
+#define FRM_MAX_FRAMES_IN_FLIGHT 4u
 
 /* Work counters of one render (exact; equal to the CPU oracle's counts). */
 typedef struct frm_stats {
@@ -140,7 +150,8 @@ int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters);
 
 /* ---- draw (replaces Graphics::render, graphics.rs:91-110). One full frame into
  *      the context framebuffer. stats == NULL: asynchronous. stats != NULL: waits
- *      for the frame and fills the counters and kernel time. */
+ *      for every frame in flight, then for this one, and fills the counters and
+ *      kernel time. */
 int frm_render(frm_ctx* ctx, frm_stats* stats);
 
 /* ---- readback (replaces the blit pass + present, graphics.rs:101-108). Copies the
@@ -183,7 +194,9 @@ int frm_reload(frm_ctx* ctx, const char* source_dir);
  *      memory of this context's GPU), each row 4*width bytes. `stream` is a
  *      hipStream_t (NULL = context stream). dev_counters, if not NULL, is device
  *      memory of FRM_NUM_COUNTERS uint64 to which the work counters are ADDED.
- *      Asynchronous. */
+ *      Asynchronous. With frames_in_flight = F the launch uses the next of F scratch
+ *      slots; a slot last used on another stream is awaited on the device, so a caller
+ *      that rotates F streams (and F destination buffers) overlaps F launches. */
 #define FRM_NUM_COUNTERS 8u
 int frm_band_rows_for(uint32_t height, uint32_t band_rows, uint32_t first_band,
                       uint32_t band_stride, uint32_t* out_rows);

@@ -31,7 +31,7 @@ def test_every_declared_symbol_is_exported(frm_lib):
 
 
 def test_abi_version(frm_lib):
-    assert frm_lib.frm_abi_version() == 1
+    assert frm_lib.frm_abi_version() == 2
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -69,7 +69,7 @@ def test_errors_are_codes_not_crashes(frm_lib):
     assert L.frm_band_rows_for(0, 4, 0, 1, ctypes.byref(out)) == _lib.FRM_ERR_INVALID_ARGUMENT
     assert L.frm_destroy(None) == _lib.FRM_OK
     ctx = ctypes.c_void_p()
-    bad = _lib.FrmConfig(0, 0, 0, 7)  # reserved must be 0
+    bad = _lib.FrmConfig(0, 0, 0, _lib.FRM_MAX_FRAMES_IN_FLIGHT + 1)  # frames_in_flight above the cap
     assert L.frm_create(ctypes.byref(ctx), ctypes.byref(bad)) == _lib.FRM_ERR_INVALID_ARGUMENT
 
 

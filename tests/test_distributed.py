@@ -1,7 +1,8 @@
 """Row-tiled multi-rank pipeline (frm.distributed.RowTiledFrame, the code bench.py runs
 over RCCL) with world_size 2 on gloo, bands rendered by the CPU oracle: the gathered frame
 equals the single-process frame byte for byte (tiling invariance) and the summed work
-counters equal the full frame's."""
+counters equal the full frames', with one and with several frames in flight; every frame
+has its own time, so a frame assembled from the wrong buffers would show."""
 import os
 import socket
 import sys
@@ -21,7 +22,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, W, H, band_rows, q):
+def _times():
+    import frm
+    return [frm.POWER8_TIME + 0.75 * k for k in range(3)]  # a different frame each time
+
+
+def _worker(rank, world, port, W, H, band_rows, inflight, q):
     for p in (ROOT, os.path.join(ROOT, "fractal-ray-marching_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     import frm
@@ -31,10 +37,15 @@ def _worker(rank, world, port, W, H, band_rows, q):
     from oracle import frm_oracle
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    p = params_for(18, 8, frm.POWER8_TIME, W, H)
+    state = {"p": None}
     counters = np.zeros(8, np.int64)
 
-    def render_bands(buf, br, first, stride):
+    def before_frame(k):
+        state["p"] = params_for(18, 8, _times()[k], W, H)
+
+    def render_bands(buf, br, first, stride, slot):
+        assert 0 <= slot < inflight
+        p = state["p"]
         rows = tiling.global_rows(H, br, first, stride)
         valid = [y for y in rows if y >= 0]
         r = frm_oracle.render(p, W, H, 128, rows=valid, threads=2)
@@ -42,13 +53,13 @@ def _worker(rank, world, port, W, H, band_rows, q):
         out[:len(valid)] = r["rgba"]  # padding rows (y < 0) are only at the end
         counters[:] += r["counters"].astype(np.int64)
 
-    def unshuffle(gathered, frame):
+    def unshuffle(gathered, frame, slot):
         g = gathered.numpy().reshape(world, -1, W, 4)
         frame.numpy()[:] = tiling.unshuffle(g, H, br_used, world).reshape(-1)
 
     br_used = band_rows
-    tf = RowTiledFrame(W, H, rank, world, band_rows, "cpu", render_bands, unshuffle)
-    tf.run(3)
+    tf = RowTiledFrame(W, H, rank, world, band_rows, "cpu", render_bands, unshuffle, inflight=inflight)
+    tf.run(3, before_frame)
     c = torch.from_numpy(counters.copy())
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     if rank == 0:
@@ -57,25 +68,26 @@ def _worker(rank, world, port, W, H, band_rows, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W,H,band_rows", [(48, 27, 4), (40, 24, 6)])
-def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows):
+@pytest.mark.parametrize("W,H,band_rows,inflight", [(48, 27, 4, 1), (40, 24, 6, 1), (48, 27, 4, 2),
+                                                    (40, 24, 6, 3)])
+def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows, inflight):
     from helpers import params_for
     import frm
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, inflight, q)) for r in range(2)]
     for pr in procs:
         pr.start()
     frame, counters, frames = q.get(timeout=180)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
-    ref = oracle.render(params_for(18, 8, frm.POWER8_TIME, W, H), W, H, 128)
-    assert np.array_equal(frame.reshape(H, W, 4), ref["rgba"])
+    refs = [oracle.render(params_for(18, 8, t, W, H), W, H, 128) for t in _times()]
+    assert np.array_equal(frame.reshape(H, W, 4), refs[-1]["rgba"])  # the last frame
     assert frames == 3
-    assert [int(v) for v in counters] == [3 * int(v) for v in ref["counters"]]
+    assert [int(v) for v in counters] == [sum(int(r["counters"][i]) for r in refs) for i in range(8)]
 
 
 def test_tiling_geometry_roundtrip():

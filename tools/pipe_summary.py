@@ -1,0 +1,8 @@
+import json, sys
+for l in sys.stdin:
+    try:
+        d = json.loads(l)
+    except Exception:
+        continue
+    print(d["workload"], d["ranks"], d["inflight"], d.get("mode"), d.get("events"), d.get("cumask"),
+          round(d["ms_per_frame"], 3), round(d["gsteps"], 2))

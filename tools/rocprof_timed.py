@@ -1,30 +1,52 @@
-"""Per-kernel average duration over the LAST k dispatches of a rocprofv3 kernel trace (the
-bench's timed region: `bench.py --steps k` runs warmup frames first), to compare with
-bench.py's live HIP-event roofline.avg_kernel_ms (which brackets sort + march + shade)."""
+"""Per-frame device time of the LAST k frames of a rocprofv3 kernel trace (the bench's timed
+region: `bench.py --steps k` runs warmup frames first), to compare with bench.py's live
+HIP-event roofline.avg_kernel_ms.
+
+With frames in flight (bench.py --inflight F > 1) the frames' kernels overlap, so the
+per-frame time is the SPAN of the last k frames' dispatches (first start to last end) / k,
+which is what bench.py's events measure; the per-kernel average durations are printed too
+(a persistent march dispatch then also holds the time it shares the GPU with its
+neighbours)."""
 import collections
 import csv
 import sys
 
 
+def kind(n):
+    return ("march_persistent" if "march_persistent" in n else "shade_pass" if "shade_pass" in n
+            else "radix_sort" if "radix_sort" in n else None)
+
+
 def main(trace, k):
-    per = collections.defaultdict(list)
+    rows = []
     for r in csv.DictReader(open(trace)):
-        n = r["Kernel_Name"]
-        name = ("march_persistent" if "march_persistent" in n else "shade_pass" if "shade_pass" in n
-                else "radix_sort" if "radix_sort" in n else None)
+        name = kind(r["Kernel_Name"])
         if name:
-            per[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    rows.sort()
+    per = collections.defaultdict(list)
+    for s, e, name in rows:
+        per[name].append((e - s) / 1e6)
+    calls = len(per["march_persistent"])
     total = 0.0
     for name in ("march_persistent", "radix_sort", "shade_pass"):
         d = per.get(name, [])
-        calls = len(per["march_persistent"])
-        # radix sort: several dispatches per frame; take the frames' share
-        per_frame = len(d) // max(calls, 1) if calls else 1
+        per_frame = len(d) // max(calls, 1) if calls else 1  # radix sort: several dispatches per frame
         last = d[-k * max(per_frame, 1):]
         avg = sum(last) / k if last else 0.0
         total += avg
         print(f"{name:18s} last {k} frames: {avg:.3f} ms per frame ({len(d)} dispatches in the trace)")
-    print(f"{'sum':18s} {total:.3f} ms per frame")
+    print(f"{'sum':18s} {total:.3f} ms per frame (sum of dispatch durations)")
+    # span: from the first dispatch of the first timed frame's march (minus its sort) to the
+    # end of the last dispatch
+    marches = [(s, e) for s, e, n in rows if n == "march_persistent"]
+    if len(marches) >= k:
+        first = marches[-k][0]
+        sorts_before = [s for s, e, n in rows if n == "radix_sort" and s <= first]
+        t0 = sorts_before[-1] if sorts_before else first
+        t0 = min([t0] + [s for s, e, n in rows if s >= t0])
+        t1 = max(e for s, e, n in rows if s >= t0)
+        print(f"{'span':18s} {(t1 - t0) / 1e6 / k:.3f} ms per frame (first start to last end of the last {k} frames)")
 
 
 if __name__ == "__main__":
