@@ -19,20 +19,23 @@ from . import tiling
 
 class RowTiledFrame:
     def __init__(self, width, height, rank, world, band_rows, device, render_bands, unshuffle,
-                 group=None, inflight=1, streams=None):
+                 group=None, inflight=1, streams=None, collective=None):
         """render_bands(buf, band_rows, first_band, band_stride, slot): enqueue the render of
         this rank's bands into the uint8 tensor buf (device memory for the GPU path) for
         frame slot `slot` (k % inflight; the GPU path renders it on streams[slot]).
         unshuffle(gathered, frame, slot): rank 0 only; rank-major band buffers -> row-major
         frame. inflight = frames in flight: frame k's render, gather and unshuffle are
         enqueued on streams[k % inflight] (torch streams; None = the current stream, as in
-        the CPU tests), so up to `inflight` frames overlap on the GPU."""
+        the CPU tests), so up to `inflight` frames overlap on the GPU. collective: gather
+        through torch.distributed (default: when world > 1; True with world 1 runs the
+        same gather/unshuffle path on one rank, a test hook for RCCL on one GPU)."""
         self.width, self.height = width, height
         self.rank, self.world = rank, world
         self.band_rows = band_rows
         self.render_bands = render_bands
         self.unshuffle = unshuffle
         self.group = group
+        self.collective = world > 1 if collective is None else bool(collective)
         self.inflight = max(1, inflight)
         self.streams = streams
         if streams is not None and len(streams) != self.inflight:
@@ -42,11 +45,11 @@ class RowTiledFrame:
         # buffer k % nbuf serves frame k. Reuse is safe in stream order: frame k + nbuf runs
         # on frame k's stream (nbuf is a multiple of inflight), after frame k's gather wait
         # and unshuffle, which _finish(k) enqueues before frame k + nbuf is issued.
-        nbuf = self.inflight if self.inflight > 1 else (2 if world > 1 else 1)
+        nbuf = self.inflight if self.inflight > 1 else (2 if self.collective else 1)
         self.nbuf = nbuf
         self.bufs = [torch.zeros(self.nbytes, dtype=torch.uint8, device=device) for _ in range(nbuf)]
         self.gathered = self.frames = None
-        if world > 1 and rank == 0:
+        if self.collective and rank == 0:
             self.gathered = [torch.zeros(world * self.nbytes, dtype=torch.uint8, device=device)
                              for _ in range(nbuf)]
             self.frames = [torch.zeros(height * width * 4, dtype=torch.uint8, device=device)
@@ -63,7 +66,7 @@ class RowTiledFrame:
         buf = self.bufs[k % self.nbuf]
         with self._stream(k):
             self.render_bands(buf, self.band_rows, self.rank, self.world, k % self.inflight)
-            if self.world == 1:
+            if not self.collective:
                 return None
             glist = None
             if self.rank == 0:
@@ -98,6 +101,6 @@ class RowTiledFrame:
 
     def output(self):
         """Rank 0: the last frame, flat RGBA8 (the band buffer itself when world == 1)."""
-        if self.world == 1:
+        if not self.collective:
             return self.bufs[self.last]
         return self.frames[self.last]

@@ -81,3 +81,51 @@ def test_render_read_frame_sees_last_frame(frm_lib, oracle, refs, flags):
         for _ in range(4):
             r.render(stats=False)
         assert np.array_equal(r.read_frame(), oracle.render(p, W // 2, H, 256)["rgba"])
+
+
+def test_rccl_gather_pipeline_one_rank(frm_lib, refs):
+    """bench.py's N>1 data path on real RCCL, with the one rank a single GPU allows (RCCL
+    refuses two ranks on one device): RowTiledFrame renders on 3 rotating streams, gathers
+    through ProcessGroupNCCL (async, stream-ordered waits) and unshuffles on the GPU. Every
+    frame has its own Parameters; the last assembled frame must equal the oracle's."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from frm.distributed import RowTiledFrame
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        F, band_rows = 3, 16
+        streams = [torch.cuda.Stream(device=dev) for _ in range(F)]
+        counters = torch.zeros(8, dtype=torch.int64, device=dev)
+        with frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL,
+                          frames_in_flight=F) as r:
+            r.resize(W, H)
+
+            def render_bands(buf, br, first, stride, slot):
+                r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, streams[slot].cuda_stream,
+                               counters.data_ptr())
+
+            def unshuffle(gathered, frame, slot):
+                r.unshuffle_bands(gathered.data_ptr(), gathered.numel(), frame.data_ptr(), frame.numel(),
+                                  band_rows, 1, streams[slot].cuda_stream)
+
+            tf = RowTiledFrame(W, H, 0, 1, band_rows, dev, render_bands, unshuffle, inflight=F, streams=streams,
+                               collective=True)
+            n = 7
+            tf.run(n, lambda k: r.update_parameters_buffer(frame_params(k)))
+            torch.cuda.synchronize()
+            img = tf.output().cpu().numpy().reshape(H, W, 4)
+            assert np.array_equal(img, refs[(n - 1) % len(FRAMES)]["rgba"])
+            c = [int(v) for v in counters.cpu().tolist()]
+            assert c[2] == sum(int(refs[k % len(FRAMES)]["counters"][2]) for k in range(n))
+    finally:
+        dist.destroy_process_group()
