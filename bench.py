@@ -122,18 +122,28 @@ def cpu_baseline(params, w, seconds):
     }
 
 
-def pmc_traffic(workload, world):
-    """HBM bytes per launch of the dominant kernel (march_persistent) from the committed
-    rocprofv3 --pmc passes of this workload (tools/pmc.sh + tools/pmc_summary.py: separate
-    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled and KiB -> B per
-    MI355X_MICROARCH.md). PMC collection needs its own profiler passes, so bench.py reports
-    the committed measurement and names it; None when there is none for this workload."""
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def pmc_summary(workload, world):
+    """Hardware counters of the dominant kernel (march_persistent) from the committed
+    rocprofv3 --pmc passes of this workload (tools/pmc.sh + tools/pmc_summary.py: one
+    counter group per pass; FETCH_SIZE doubled and KiB -> B per MI355X_MICROARCH.md).
+    PMC collection needs its own profiler passes (they serialise the kernels), so bench.py
+    reports the committed measurement and names it; None when there is none."""
     path = os.path.join(ROOT, "profiles", "round1", f"pmc_{workload}_march.json")
     if world != 1 or not os.path.exists(path):
-        return None, None
+        return None
     with open(path) as fh:
         s = json.load(fh)
-    return s["hbm_read_bytes"] + s["hbm_write_bytes"], os.path.relpath(path, ROOT)
+    return {
+        "traffic": s["hbm_read_bytes"] + s["hbm_write_bytes"],
+        "valu_busy": s["valu_busy"],
+        "valu_lane_utilization": s["valu_lane_utilization"],
+        "hbm_write_gbps": s["hbm_write_gbps"],
+        "hbm_write_frac": s["hbm_write_gbps"] / HBM_PEAK_GBPS,
+        "source": os.path.relpath(path, ROOT),
+    }
 
 
 def main():
@@ -272,7 +282,7 @@ def main():
         avg_kernel_s = span_ms / 1e3 / args.steps
         wom_per_launch = st["wom_ops"] / args.steps / world
         achieved = wom_per_launch / avg_kernel_s / 1e12
-        traffic, traffic_src = pmc_traffic(args.workload, world)
+        pmc = pmc_summary(args.workload, world) or {}
         out = {
             "metric": METRIC,
             "value": steps_total / elapsed / 1e9,
@@ -305,8 +315,14 @@ def main():
                 "peak": VALU_PEAK_TOPS,
                 "unit": "Tlane-op/s",
                 "frac": achieved / VALU_PEAK_TOPS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
+                "traffic": pmc.get("traffic"),
+                "traffic_source": pmc.get("source"),
+                # rocprofv3 hardware view of the same kernel (committed PMC passes):
+                # SQ VALU-busy, active-lane fraction, HBM write rate against the 8 TB/s peak
+                "valu_busy": pmc.get("valu_busy"),
+                "valu_lane_utilization": pmc.get("valu_lane_utilization"),
+                "hbm_write_gbps": pmc.get("hbm_write_gbps"),
+                "hbm_write_frac": pmc.get("hbm_write_frac"),
                 "kernel": "frm::render",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "avg_launch_ms": launch_ms,

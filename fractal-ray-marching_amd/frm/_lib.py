@@ -22,7 +22,7 @@ FRM_ERR_UNSUPPORTED = 7
 FRM_ERR_COMPILE = 8
 
 FRM_NUM_SCENES = 19
-FRM_MAX_FRAMES_IN_FLIGHT = 4
+FRM_MAX_FRAMES_IN_FLIGHT = 8
 FRM_DEFAULT_MAX_STEPS = 5000
 FRM_MAX_NUM_ITERATIONS = 4096
 FRM_NUM_COUNTERS = 8

@@ -112,7 +112,7 @@ typedef struct frm_config {
                          reference renders one frame per submit (graphics.rs:91-110).        */
 } frm_config;
 
-#define FRM_MAX_FRAMES_IN_FLIGHT 4u
+#define FRM_MAX_FRAMES_IN_FLIGHT 8u
 
 /* Work counters of one render (exact; equal to the CPU oracle's counts). */
 typedef struct frm_stats {

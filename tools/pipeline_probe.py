@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--events", default="0")
     ap.add_argument("--cumask", default="0")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--rank-ids", default="0", help="ranks whose share to time ('all' = every rank)")
     args = ap.parse_args()
     for wl in args.workloads.split(","):
         for P in [int(x) for x in args.ranks.split(",")]:
@@ -98,8 +99,10 @@ def main():
                 for m in args.modes.split(","):
                     for ev in [bool(int(x)) for x in args.events.split(",")]:
                         for cm in [bool(int(x)) for x in args.cumask.split(",")]:
-                            for _ in range(args.repeat):
-                                print(json.dumps(run(wl, P, 0, F, args.frames, 2, m, ev, cm)), flush=True)
+                            ids = range(P) if args.rank_ids == "all" else [int(x) for x in args.rank_ids.split(",") if int(x) < P]
+                            for rk in ids:
+                                for _ in range(args.repeat):
+                                    print(json.dumps(run(wl, P, rk, F, args.frames, 2, m, ev, cm)), flush=True)
 
 
 if __name__ == "__main__":

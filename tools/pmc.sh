@@ -3,7 +3,7 @@
 # Usage: OUT=gpurun_out/pmc ARGS="--steps 2 --warmup 1" bash tools/pmc.sh
 set -o pipefail
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${ARGS:---steps 4 --warmup 2 --no-cpu-baseline}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true

@@ -12,6 +12,9 @@ import sys
 
 
 KERNEL = "march_persistent"
+# dispatches skipped at the start: the first launch of each frames-in-flight slot has no
+# scheduling history (row-major fetch order) and is not the steady state bench.py times
+SKIP = 2
 
 
 def load(d, name):
@@ -22,11 +25,12 @@ def load(d, name):
     for r in csv.DictReader(open(files[0])):
         if KERNEL in r["Kernel_Name"]:
             agg[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-    # average over the dispatches of the render kernel
+    # average over the steady-state dispatches of the render kernel
+    keep = sorted(agg)[SKIP:] or sorted(agg)
     out = collections.defaultdict(float)
-    for c in agg.values():
-        for k, v in c.items():
-            out[k] += v / len(agg)
+    for i in keep:
+        for k, v in agg[i].items():
+            out[k] += v / len(keep)
     return dict(out)
 
 
@@ -38,7 +42,9 @@ def main(d):
     dur = []
     for r in csv.DictReader(open(trace[0])):
         if KERNEL in r["Kernel_Name"]:
-            dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+            dur.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
+    dur = [d for _, d in sorted(dur)]
+    dur = dur[SKIP:] or dur
     t = sum(dur) / len(dur)
     grbm_xcd = c["GRBM_GUI_ACTIVE"] / 8
     s = {
