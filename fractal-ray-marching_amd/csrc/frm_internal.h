@@ -40,6 +40,12 @@ struct KernelArgs {
   uint8_t* pixel_key;             // persistent kernel: cost key per local pixel (out)
 };
 
+#ifndef FRM_MARCH_BLOCK
+#define FRM_MARCH_BLOCK 256
+#endif
+constexpr uint32_t kMarchBlock = FRM_MARCH_BLOCK;  // march_persistent threads per workgroup
+constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
+
 #if !defined(__HIPCC_RTC__)  // host-side launchers; hiprtc only needs the types above
 // Render kernels compiled at run time from edited sources (frm_reload.hip), per DE family
 // (Family in frm_scene.h) and ITERS.

@@ -107,7 +107,7 @@ hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, 
 static int blocks_override() {  // experiments: FRM_BLOCKS_PER_CU
   const char* env = getenv("FRM_BLOCKS_PER_CU");
   const int v = env ? atoi(env) : 0;
-  return v >= 1 && v <= 16 ? v : 0;
+  return v >= 1 && v <= 64 ? v : 0;
 }
 
 // A reloaded module's kernel (frm_reload.hip) takes the same KernelArgs by value.
@@ -122,7 +122,7 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   static int blocks_per_cu = 0;  // occupancy of this instantiation (per process)
   if (blocks_per_cu == 0) {
     int n = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS>, 256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS>, kMarchBlock, 0);
     if (e != hipSuccess) return e;
     blocks_per_cu = n > 0 ? n : 1;
   }
@@ -130,16 +130,16 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   if (const int v = blocks_override()) bpc = v;
   // every wave starts with one chunk of 64 pixels; never launch more waves than chunks
   uint32_t blocks = (uint32_t)(bpc * cu_count);
-  const uint32_t max_blocks = ((args.npix + kChunk - 1u) / kChunk + 3u) / 4u;
+  const uint32_t max_blocks = ((args.npix + kChunk - 1u) / kChunk + kMarchWaves - 1u) / kMarchWaves;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) blocks = 1;
   const uint32_t pixels = args.g.local_rows * args.f.width;
   if (rk) {
-    hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(256), stream, args);
+    hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(kMarchBlock), stream, args);
     if (e != hipSuccess) return e;
     return module_launch(rk->shade[FAM], dim3((pixels + 255u) / 256u), dim3(256), stream, args);
   }
-  hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(256), 0, stream, args);
+  hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
   hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u), dim3(256), 0, stream, args);
   return hipGetLastError();
 }

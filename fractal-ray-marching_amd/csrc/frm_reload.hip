@@ -122,7 +122,7 @@ int compile_reloaded(const char* dir, int device, ReloadedKernels** out, std::st
         } else {
           rk->persistent[f][it] = fn;
           int n = 0;
-          (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, 0);
+          (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kMarchBlock, 0);
           rk->persistent_blocks_per_cu[f][it] = n > 0 ? n : 1;
         }
       }

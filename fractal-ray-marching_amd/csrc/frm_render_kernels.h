@@ -73,6 +73,7 @@ __global__ __launch_bounds__(256) void render_simple(KernelArgs a) {
 constexpr uint32_t kIdle = 0xFFFFFFFFu;
 constexpr uint32_t kChunk = 64u;  // pixels per queue fetch (one per lane of the fetching wave)
 
+
 enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -95,8 +96,8 @@ template <uint32_t FAM, bool ITERS>
 #ifndef FRM_MARCH_WAVES_PER_SIMD
 #define FRM_MARCH_WAVES_PER_SIMD 1
 #endif
-__global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
-  __shared__ float4 chunk_rays[4][kChunk];  // per wave: camera ray xyz + local pixel index bits
+__global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
+  __shared__ float4 chunk_rays[kMarchWaves][kChunk];  // per wave: camera ray xyz + local pixel index bits
 
   const FrameUniforms& f = a.f;
   const SceneUniforms& su = a.s;
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(256, FRM_MARCH_WAVES_PER_SIMD) void march_persisten
     atomicMax(a.debug + 4, (unsigned long long)__builtin_amdgcn_s_memrealtime());  // last wave end
   }
   {
-    const uint32_t w = blockIdx.x * 4u + wave;
+    const uint32_t w = blockIdx.x * kMarchWaves + wave;
     uint32_t hw = 0;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     if (lane == 0 && w < kWaveDebugSlots) {
