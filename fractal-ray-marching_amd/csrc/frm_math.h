@@ -147,13 +147,14 @@ FRM_HD float log2_(float x) {
   float r = fma_(log1p_kernel_(f), kLog2e, fe);
   return log_special_(x, r);
 }
-FRM_HD float log_(float x) {
+// log_ for positive finite x (normal or subnormal), where log_special_ changes nothing.
+FRM_HD float log_posfinite_(float x) {
   float f, fe;
   log_split_(x, &f, &fe);
   float l = log1p_kernel_(f);
-  float r = fma_(fe, 0.693359375f, fma_(fe, -2.12194440e-4f, l));
-  return log_special_(x, r);
+  return fma_(fe, 0.693359375f, fma_(fe, -2.12194440e-4f, l));
 }
+FRM_HD float log_(float x) { return log_special_(x, log_posfinite_(x)); }
 
 // ---- exp2 / pow -------------------------------------------------------------
 // k = rint(y) after clamping y to [-151, 129]; f = y - k in [-1/2, 1/2] (exact);

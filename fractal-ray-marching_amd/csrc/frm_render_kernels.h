@@ -177,11 +177,16 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     //    shadow ray) and the record store of a finished pixel are branches.
     const bool cons = pix != kIdle && done;
     bool ev_bail = false;
+    // the distance's log without its special-value selects when no consuming lane has a
+    // magnitude that is 0, negative, infinite or NaN (wave-uniform test; same bits)
+    bool plain_log = true;
+    if constexpr (FAM == kMandelbulb)
+      plain_log = ballot(cons && !__builtin_amdgcn_classf(mag, 0x180 /* +subnormal, +normal */)) == 0;
     if (cons) {
       done = false;
       if constexpr (FAM == kMandelbulb) {
         FRM_SUB_BEGIN();
-        de = mb_distance(mag, dr);
+        de = plain_log ? mb_distance_posfinite(mag, dr) : mb_distance(mag, dr);
         acc_body += body;          // bodies this DE ran (N+1 on a count exit)
         ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
         FRM_SUB_END(0);

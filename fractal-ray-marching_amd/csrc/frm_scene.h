@@ -188,6 +188,8 @@ FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 }
 // distance = 0.5 * log(magnitude) * magnitude / magnitude_derivative, fragment.wgsl:269
 FRM_HD float mb_distance(float r, float dr) { return ((0.5f * log_(r)) * r) / dr; }
+// mb_distance for positive finite r (log_'s special-value selects cannot fire): same bits.
+FRM_HD float mb_distance_posfinite(float r, float dr) { return ((0.5f * log_posfinite_(r)) * r) / dr; }
 
 #if defined(__HIPCC__)
 // Lane mask of a per-lane predicate (no int round trip, unlike HIP's __ballot(int)).
