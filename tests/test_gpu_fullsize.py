@@ -15,6 +15,15 @@ import frm
 pytestmark = pytest.mark.gpu
 
 THREADS = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share
+_ORACLE = {}  # whole-frame oracle renders, shared by the tests of this module
+
+
+def oracle_frame(oracle, name):
+    if name not in _ORACLE:
+        w = frm.WORKLOADS[name]
+        p = frm.make_parameters(w, pose="P1")
+        _ORACLE[name] = oracle.render(p, w.width, w.height, w.max_steps, threads=THREADS)
+    return _ORACLE[name]
 
 
 def counters_of(st):
@@ -40,7 +49,7 @@ def test_full_frame_bit_exact(frm_lib, oracle, name):
     w = frm.WORKLOADS[name]
     p = frm.make_parameters(w, pose="P1")
     img, st = render_like_bench(w, p)
-    ref = oracle.render(p, w.width, w.height, w.max_steps, threads=THREADS)
+    ref = oracle_frame(oracle, name)
     diff = np.any(img != ref["rgba"], axis=-1)
     assert not diff.any(), f"{name}: {int(diff.sum())} of {w.width * w.height} pixels differ"
     assert counters_of(st) == [int(c) for c in ref["counters"]]
@@ -61,3 +70,45 @@ def test_full_size_row_sample_bit_exact(frm_lib, oracle, name, stride):
         got = img[rows]
         diff = np.any(got != ref["rgba"], axis=-1)
         assert not diff.any(), f"{name} t={t}: {int(diff.sum())} of {diff.size} sampled pixels differ"
+
+
+def test_headline_row_split_8_ranks(frm_lib, oracle):
+    """bench.py's default 8-GPU data path, simulated on one device: 8 contexts render their
+    interleaved 18-row bands of the 4K headline (three frames in flight each, so the
+    scheduled order runs), frm_unshuffle_bands reassembles rank-major buffers into the frame,
+    which equals the oracle's; the summed counters equal the whole frame's."""
+    import torch
+
+    from frm import tiling
+
+    w = frm.WORKLOADS["HEADLINE"]
+    ranks = 8
+    p = frm.make_parameters(w, pose="P1")
+    band_rows = tiling.choose_band_rows(w.height, ranks)
+    rows = tiling.rank_buffer_rows(w.height, band_rows, ranks)
+    rank_stride = rows * w.width * 4
+    dev = torch.device("cuda", 0)
+    gathered = torch.zeros(ranks * rank_stride, dtype=torch.uint8, device=dev)
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    rds = [frm.Renderer(device=0, max_steps=w.max_steps, frames_in_flight=3) for _ in range(ranks)]
+    try:
+        for rd in rds:
+            rd.resize(w.width, w.height)
+            rd.update_parameters_buffer(p)
+        for frame in range(3):
+            counters.zero_()
+            for r, rd in enumerate(rds):
+                view = gathered[r * rank_stride:(r + 1) * rank_stride]
+                rd.render_bands(view.data_ptr(), rank_stride, band_rows, r, ranks, 0, counters.data_ptr())
+            torch.cuda.synchronize()
+        out = torch.zeros(w.width * w.height * 4, dtype=torch.uint8, device=dev)
+        rds[0].unshuffle_bands(gathered.data_ptr(), rank_stride, out.data_ptr(), out.numel(), band_rows, ranks)
+        torch.cuda.synchronize()
+        img = out.cpu().numpy().reshape(w.height, w.width, 4)
+        ref = oracle_frame(oracle, "HEADLINE")
+        diff = np.any(img != ref["rgba"], axis=-1)
+        assert not diff.any(), f"{int(diff.sum())} pixels differ"
+        assert [int(v) for v in counters.cpu().tolist()][:7] == [int(v) for v in ref["counters"][:7]]
+    finally:
+        for rd in rds:
+            rd.close()
