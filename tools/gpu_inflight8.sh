@@ -1,3 +1,4 @@
+# frames in flight up to 8 and all 8 ranks' shares of an 8-way split (pipeline_probe)
 set -o pipefail
 O=gpurun_out/inflight8
 mkdir -p $O
