@@ -111,6 +111,9 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   uint32_t slots_used = kChunk;
   bool exhausted = false;
   uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
+#ifdef FRM_COUNT_EXACT
+  uint64_t n_dbg_total = 0, n_dbg_exact = 0;
+#endif
 
   // per-lane state
   uint32_t pix = kIdle;      // local pixel index (lr * width + x) being marched
@@ -154,6 +157,10 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 #endif
         uint32_t fin = 0;
         if (lane_in(pending)) {
+#if defined(FRM_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostic: body-loop iterations, and those that ran the exact body
+          n_dbg_total++;
+          if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
+#endif
           mb_step(su, q, mag, z, dr);
           body++;
           if (body > n_iter) {
@@ -364,6 +371,9 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   }
 #endif
   if (lane == 0) {
+#ifdef FRM_COUNT_EXACT
+    atomicAdd(&a.counters[7], (unsigned long long)((n_dbg_total << 32) | n_dbg_exact));
+#endif
     unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll
     for (int k = 0; k < 7; ++k)
