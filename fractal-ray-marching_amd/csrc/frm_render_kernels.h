@@ -122,8 +122,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   v3 o = mk(0.f, 0.f, 0.f), d = o, nsum = o, q = o, z = o;
   float t = 0.f, closeness = 0.f, dr = 1.f, mag = 0.f, de = 0.f;
   uint32_t it = 0, psteps = 0, body = 0;
-  uint32_t acc_body = 0;   // per-lane Mandelbulb bodies (other families: DEs, for scheduling)
-  uint32_t pix_body0 = 0;  // acc_body when the lane's pixel started
+  uint32_t pix_cost = 0;  // the lane's pixel's Mandelbulb bodies (other families: DEs) so far, for
+                          // its scheduling key; the wave's body total is counted in SGPRs
 #ifdef FRM_STAMPS
   uint64_t stamp_service = 0, n_service = 0, n_loop = 0, real_exhaust = 0;
   uint64_t stamp_consume = 0, stamp_refill = 0, n_fetch = 0;
@@ -152,6 +152,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       const uint64_t waitable = exhausted ? live : ~0ull;
       for (;;) {
         if (pending == 0 || (uint32_t)__popcll(waitable & ~pending) >= a.service_min) break;
+        n_body += (uint64_t)__popcll(pending);  // one body per computing lane this iteration
 #ifdef FRM_STAMPS
         n_loop++;
 #endif
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       if constexpr (FAM == kMandelbulb) {
         FRM_SUB_BEGIN();
         de = plain_log ? mb_distance_posfinite(mag, dr) : mb_distance(mag, dr);
-        acc_body += body;          // bodies this DE ran (N+1 on a count exit)
+        pix_cost += body;          // bodies this DE ran (N+1 on a count exit)
         ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
         FRM_SUB_END(0);
       }
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       FRM_SUB_BEGIN();
       const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
       *reinterpret_cast<uint4*>(&rec[pix].closeness) =
-          make_uint4(__float_as_uint(closeness), psteps, flags, cost_key(acc_body - pix_body0));
+          make_uint4(__float_as_uint(closeness), psteps, flags, cost_key(pix_cost));
       pix = kIdle;
       FRM_SUB_END(3);
     }
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           const float4 r = chunk_rays[wave][slot];
           pix = __float_as_uint(r.w);
           if (pix != kIdle) {
-            pix_body0 = acc_body;
+            pix_cost = 0;
             d = mk(r.x, r.y, r.z);
             o = f.origin;
             t = 0.f;
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
         DeCount unused = {0u, 0u};
         de = scene_de<FAM, ITERS>(su, q, unused);
         done = true;
-        acc_body++;  // fixed-trip families: the scheduling cost unit is one DE
+        pix_cost++;  // fixed-trip families: the scheduling cost unit is one DE
       }
     }
 
@@ -340,7 +341,6 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     if (exhausted && ballot(pix != kIdle) == 0) break;
   }
 
-  if constexpr (FAM == kMandelbulb) n_body = wave_sum(acc_body);
 #ifdef FRM_STAMPS
   if (lane == 0) {
     atomicAdd(&a.counters[7], (unsigned long long)stamp_service);
