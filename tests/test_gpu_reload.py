@@ -87,3 +87,22 @@ def test_reload_error_keeps_previous_kernels(gpu_renderer_factory, oracle, tmp_p
         r.update_parameters_buffer(p)
         r.render()
         assert np.array_equal(r.read_frame(), ref["rgba"])
+
+
+def test_reload_with_frames_in_flight(frm_lib, oracle, tmp_path):
+    """Reloaded kernels with 3 frames in flight: consecutive frames with their own parameters
+    render on rotating slots through hipModuleLaunchKernel; every frame equals the oracle's
+    (frm_render with stats waits for every slot, so each frame is read back alone)."""
+    src = copy_sources(tmp_path, "csrc")
+    frames = [params_for(18, 6, frm.POWER8_TIME, 96, 54, pose=pose) for pose in ("P0", "P1", "P2")]
+    frames += [params_for(0, 3, 0.0, 96, 54), params_for(18, 4, 1.5, 96, 54)]
+    refs = [oracle.render(p, 96, 54, 256)["rgba"] for p in frames]
+    with frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL, frames_in_flight=3) as r:
+        r.resize(96, 54)
+        r.reload(str(src))
+        for rounds in range(2):
+            for p, ref in zip(frames, refs):
+                r.update_parameters_buffer(p)
+                r.render(stats=False)
+                r.render(stats=False)  # a second frame in flight of the same parameters
+                assert np.array_equal(r.read_frame(), ref)
