@@ -69,8 +69,8 @@ def parse():
                     "whole frames of an orbit fly-through (no data-path collective, weak scaling)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU (frm_config.frames_in_flight): frame k+1 renders "
-                    "while frame k's longest pixels finish; 1 = one frame at a time; 0 = 2 for whole "
-                    "frames, 3 for a rank's bands of a split frame (measured best, DESIGN.md)")
+                    "while frame k's longest pixels finish; 1 = one frame at a time; 0 = 3 for a rank's "
+                    "bands of a split frame and frames below 4 M pixels, else 2 (measured best, DESIGN.md)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
@@ -187,7 +187,12 @@ def main():
     flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
         {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel])
     split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
-    inflight = args.inflight or (2 if split == 1 else 3)
+    band_rows = args.band_rows or (w.height if split == 1 else tiling.choose_band_rows(w.height, world))
+    local_pixels = w.width * min(w.height, tiling.rank_rows(w.height, band_rows, 0 if split == 1 else rank, split))
+    # frames in flight: a frame's costliest pixels set its tail, which weighs more the fewer
+    # pixels a launch has (measured: 4K/8K whole frames best at 2, 1080p and a rank's share
+    # of a split frame at 3)
+    inflight = args.inflight or (3 if split > 1 or local_pixels < 4_000_000 else 2)
     inflight = max(1, min(inflight, frm.FRM_MAX_FRAMES_IN_FLIGHT))
     r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=inflight)
     r.resize(w.width, w.height)
@@ -195,8 +200,6 @@ def main():
     if args.reload:
         r.reload(args.reload)
 
-    band_rows = args.band_rows or (w.height if split == 1 else tiling.choose_band_rows(w.height, world))
-    local_pixels = w.width * min(w.height, tiling.rank_rows(w.height, band_rows, 0 if split == 1 else rank, split))
     kernel_used = r.kernel_for(local_pixels) + (" (auto)" if args.kernel == "auto" else "")
     dev = torch.device("cuda", local)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
