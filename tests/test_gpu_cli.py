@@ -28,13 +28,19 @@ def read_ppm(path):
     return np.frombuffer(pix, np.uint8).reshape(h, w, 3)
 
 
-def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib):
+@pytest.mark.parametrize("gpus", [0, 1], ids=["one-context", "rccl-row-tiled"])
+def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib, gpus):
+    """gpus=1: the CLI's C host multi-GPU path (ncclCommInitAll, interleaved bands per device
+    via frm_render_bands, RCCL send/recv gather on device 0, frm_unshuffle_bands) with the
+    one device this box has; N > 1 runs the same code with more ranks."""
     W, H, frames, dt, keys, orbit = 96, 54, 3, 0.05, frm.HeldKeys.MOVE_FORWARD | frm.HeldKeys.YAW_LEFT, 2.0
     pos, iters, time, steps = (1.5, 0.9, -1.5), 6, frm.POWER8_TIME, 256
     out = str(tmp_path / "f_%02d.ppm")
     cmd = [EXE, "--width", str(W), "--height", str(H), "--frames", str(frames), "--dt", str(dt),
            "--keys", str(keys), "--orbit", str(orbit), "--lock-pitch", "--pos", *map(str, pos),
            "--iters", str(iters), "--time", str(time), "--max-steps", str(steps), "--scene", "18", "--out", out]
+    if gpus:
+        cmd += ["--gpus", str(gpus)]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert res.returncode == 0, res.stderr
     lines = [json.loads(l) for l in res.stdout.splitlines() if l.startswith("{")]
@@ -59,3 +65,4 @@ def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib):
         got = read_ppm(out % fr)
         assert np.array_equal(got, ref["rgba"][..., :3]), f"frame {fr}"
         assert lines[fr]["march_steps"] == int(ref["counters"][2]) + int(ref["counters"][3])
+        assert lines[fr]["hit_pixels"] == int(ref["counters"][1])
