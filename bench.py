@@ -5,7 +5,9 @@ Workload (BASELINE.json metric): 3840x2160 Mandelbulb (scene 18 at power 8), 12 
 iterations, 256 march steps, fixed camera pose P1; one "step" = one whole frame of the
 hot path (fragment_main for every pixel) with inputs resident on the GPU.
 
-N GPUs (one process each, torch.distributed.run):
+N GPUs (one process each): launched by torch.distributed.run (the driver's multi-GPU runs),
+or, when no launcher set WORLD_SIZE, bench.py starts `torch.distributed.run` itself as a child
+process (before anything touches a GPU) and prints rank 0's line:
 * --split rows (default): every frame is split into interleaved row bands across the
   ranks, gathered to rank 0 over RCCL (xGMI) and reassembled there (frm_unshuffle_bands):
   strong scaling of the fixed-pose workload, as BASELINE.json's north star describes. A
@@ -24,9 +26,12 @@ Prints ONE JSON line on rank 0. `value` = G ray-march-steps/s of the whole job
                     [--pose P0|P1|P2] [--kernel persistent|simple] [--no-cpu-baseline]
 """
 import argparse
+import hashlib
 import math
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -132,24 +137,82 @@ def pmc_summary(workload, world):
     rocprofv3 --pmc passes of this workload (tools/pmc.sh + tools/pmc_summary.py: one
     counter group per pass; FETCH_SIZE doubled and KiB -> B per MI355X_MICROARCH.md).
     PMC collection needs its own profiler passes (they serialise the kernels), so bench.py
-    reports the committed measurement and names it; None when there is none."""
-    path = os.path.join(ROOT, "profiles", "round1", f"pmc_{workload}_march.json")
-    if world != 1 or not os.path.exists(path):
+    reports the committed measurement and names it, newest round first, and only when the
+    summary's recorded source hash equals the hash of the kernel sources being run
+    (frm.provenance): counters of an older kernel are reported as stale, never as current."""
+    from frm import provenance
+
+    if world != 1:
         return None
-    with open(path) as fh:
-        s = json.load(fh)
-    return {
-        "traffic": s["hbm_read_bytes"] + s["hbm_write_bytes"],
-        "valu_busy": s["valu_busy"],
-        "valu_lane_utilization": s["valu_lane_utilization"],
-        "hbm_write_gbps": s["hbm_write_gbps"],
-        "hbm_write_frac": s["hbm_write_gbps"] / HBM_PEAK_GBPS,
-        "source": os.path.relpath(path, ROOT),
-    }
+    cur = provenance.source_sha256()
+    stale = None
+    for rnd in ("round2", "round1"):
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_{workload}_march.json")
+        if not os.path.exists(path):
+            continue
+        with open(path) as fh:
+            s = json.load(fh)
+        if s.get("source_sha256") != cur:
+            stale = stale or os.path.relpath(path, ROOT)
+            continue
+        return {
+            "traffic": s["hbm_read_bytes"] + s["hbm_write_bytes"],
+            "valu_busy": s["valu_busy"],
+            "valu_lane_utilization": s["valu_lane_utilization"],
+            "hbm_write_gbps": s["hbm_write_gbps"],
+            "hbm_write_frac": s["hbm_write_gbps"] / HBM_PEAK_GBPS,
+            "source": os.path.relpath(path, ROOT),
+            "source_sha256": cur,
+        }
+    return {"stale": stale, "source_sha256": cur} if stale else None
+
+
+def launch_ranks(args):
+    """--gpus N > 1 with no torch.distributed.run environment: run N ranks under a child
+    `python -m torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1) and
+    forward rank 0's JSON line. This process never initialises HIP, so nothing here execs
+    over a GPU context; the child's exit status is ours."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    for ln in p.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if p.returncode != 0 or len(lines) != 1:
+        raise SystemExit(f"bench.py: {args.gpus} ranks exited with {p.returncode}, {len(lines)} result lines")
+    out = json.loads(lines[0])
+    out["launcher"] = "bench.py -> torch.distributed.run (child process)"
+    print(json.dumps(out))
+
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
+
+
+def frame_check(frame, workload, pose, animated):
+    """sha256 of the last rendered (for N>1: gathered and reassembled) frame against the
+    oracle's whole-frame golden hash (tests/golden/fullsize.json, generated on the CPU by
+    tests/golden/make_fullsize_golden.py): the output does not depend on how the frame was
+    tiled over ranks or scheduled. None when no golden frame exists for this configuration
+    (other poses; animated workloads, whose last frame's time depends on the frame count)."""
+    sha = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
+    key = f"{workload}_{pose}"
+    gold = None
+    if not animated and os.path.exists(GOLDEN):
+        with open(GOLDEN) as fh:
+            gold = json.load(fh).get(key)
+    return {"frame_sha256": sha, "frame_sha_ok": None if gold is None else sha == gold["sha256"],
+            "frame_golden": None if gold is None else f"tests/golden/fullsize.json[{key}]"}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
     import torch
     import torch.distributed as dist
 
@@ -158,6 +221,7 @@ def main():
     from frm.distributed import RowTiledFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    backend = None
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -172,6 +236,8 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = dist.get_backend()
+        comm_ranks = dist.get_world_size()
 
     w = frm.WORKLOADS[args.workload]
     params = frm.make_parameters(w, pose=args.pose)
@@ -277,6 +343,11 @@ def main():
         dist.all_reduce(stats_vec[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
     elapsed = float(stats_vec[0])
+    if world > 1:
+        # the communicator the frames actually went through: every rank reports its size
+        seen = torch.tensor([comm_ranks], dtype=torch.int64, device=dev)
+        dist.all_reduce(seen, op=dist.ReduceOp.MIN)
+        comm_ranks = int(seen)
     c = [int(v) for v in cnt.cpu().tolist()]
     st = r.stats_from_counters(c)
     steps_total = st["march_steps"]
@@ -306,7 +377,8 @@ def main():
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
                 "pose": args.pose, "frames_in_flight": inflight, "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
-                "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + RCCL gather" if split > 1 else
+                "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + "
+                                f"{'RCCL' if backend == 'nccl' else backend + ' (host-staged)'} gather" if split > 1 else
                                 f"alternate-frame rendering x{world}: rank r renders the {args.pose} view "
                                 f"rotated by r*pi/4 about +y, whole frames, no data-path collective"
                                 if world > 1 else "single GPU"),
@@ -322,6 +394,8 @@ def main():
                 "frac": achieved / VALU_PEAK_TOPS,
                 "traffic": pmc.get("traffic"),
                 "traffic_source": pmc.get("source"),
+                "pmc_source_sha256": pmc.get("source_sha256"),
+                "pmc_stale": pmc.get("stale"),
                 # rocprofv3 hardware view of the same kernel (committed PMC passes):
                 # SQ VALU-busy, active-lane fraction, HBM write rate against the 8 TB/s peak
                 "valu_busy": pmc.get("valu_busy"),
@@ -337,6 +411,11 @@ def main():
             },
             "counters": st,
         }
+        if world > 1:
+            out["comm"] = {"backend": backend, "ranks": comm_ranks,
+                           "data_path": "dist.gather of row bands to rank 0" if split > 1 else "none (timing only)"}
+            out["rccl_ranks"] = comm_ranks if backend == "nccl" else None
+        out.update(frame_check(tf.output(), args.workload, args.pose, w.animated))
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(params, w, args.cpu_seconds)
         print(json.dumps(out))

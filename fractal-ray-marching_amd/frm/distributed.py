@@ -19,7 +19,7 @@ from . import tiling
 
 class RowTiledFrame:
     def __init__(self, width, height, rank, world, band_rows, device, render_bands, unshuffle,
-                 group=None, inflight=1, streams=None, collective=None):
+                 group=None, inflight=1, streams=None, collective=None, stage_host=None):
         """render_bands(buf, band_rows, first_band, band_stride, slot): enqueue the render of
         this rank's bands into the uint8 tensor buf (device memory for the GPU path) for
         frame slot `slot` (k % inflight; the GPU path renders it on streams[slot]).
@@ -28,7 +28,11 @@ class RowTiledFrame:
         enqueued on streams[k % inflight] (torch streams; None = the current stream, as in
         the CPU tests), so up to `inflight` frames overlap on the GPU. collective: gather
         through torch.distributed (default: when world > 1; True with world 1 runs the
-        same gather/unshuffle path on one rank, a test hook for RCCL on one GPU)."""
+        same gather/unshuffle path on one rank, a test hook for RCCL on one GPU).
+        stage_host: gather through host copies of the band buffers (default: when the
+        backend is gloo and the buffers live on a GPU). A test hook: RCCL refuses two ranks
+        on one GPU, so a 1-GPU box runs the row split with gloo, whose gather takes host
+        tensors only; the RCCL path never stages."""
         self.width, self.height = width, height
         self.rank, self.world = rank, world
         self.band_rows = band_rows
@@ -40,6 +44,10 @@ class RowTiledFrame:
         self.streams = streams
         if streams is not None and len(streams) != self.inflight:
             raise ValueError(f"{len(streams)} streams for {self.inflight} frames in flight")
+        if stage_host is None:
+            stage_host = (self.collective and torch.device(device).type == "cuda"
+                          and dist.get_backend(group) == "gloo")
+        self.stage_host = bool(stage_host)
         self.rows_local = tiling.rank_buffer_rows(height, band_rows, world)
         self.nbytes = self.rows_local * width * 4
         # buffer k % nbuf serves frame k. Reuse is safe in stream order: frame k + nbuf runs
@@ -69,15 +77,24 @@ class RowTiledFrame:
             if not self.collective:
                 return None
             glist = None
+            g = self.gathered[k % self.nbuf] if self.rank == 0 else None
+            if self.stage_host:
+                host = buf.cpu()  # waits for this frame's render on the stream
+                if self.rank == 0:
+                    glist = [torch.empty_like(host) for _ in range(self.world)]
+                dist.gather(host, gather_list=glist, dst=0, group=self.group)
+                if self.rank == 0:
+                    g.copy_(torch.cat(glist))
+                return None
             if self.rank == 0:
-                g = self.gathered[k % self.nbuf]
                 glist = [g[i * self.nbytes:(i + 1) * self.nbytes] for i in range(self.world)]
             return dist.gather(buf, gather_list=glist, dst=0, group=self.group, async_op=True)
 
     def _finish(self, k, work):
-        if work is not None:
+        if self.collective:
             with self._stream(k):
-                work.wait()  # NCCL: the stream waits for the gather (the host does not)
+                if work is not None:
+                    work.wait()  # NCCL: the stream waits for the gather (the host does not)
                 if self.rank == 0:
                     self.unshuffle(self.gathered[k % self.nbuf], self.frames[k % self.nbuf],
                                    k % self.inflight)

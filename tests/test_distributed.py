@@ -27,7 +27,7 @@ def _times():
     return [frm.POWER8_TIME + 0.75 * k for k in range(3)]  # a different frame each time
 
 
-def _worker(rank, world, port, W, H, band_rows, inflight, q):
+def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None):
     for p in (ROOT, os.path.join(ROOT, "fractal-ray-marching_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     import frm
@@ -58,7 +58,9 @@ def _worker(rank, world, port, W, H, band_rows, inflight, q):
         frame.numpy()[:] = tiling.unshuffle(g, H, br_used, world).reshape(-1)
 
     br_used = band_rows
-    tf = RowTiledFrame(W, H, rank, world, band_rows, "cpu", render_bands, unshuffle, inflight=inflight)
+    tf = RowTiledFrame(W, H, rank, world, band_rows, "cpu", render_bands, unshuffle, inflight=inflight,
+                        stage_host=stage_host)
+    assert tf.stage_host == bool(stage_host)
     tf.run(3, before_frame)
     c = torch.from_numpy(counters.copy())
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
@@ -68,16 +70,18 @@ def _worker(rank, world, port, W, H, band_rows, inflight, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W,H,band_rows,inflight", [(48, 27, 4, 1), (40, 24, 6, 1), (48, 27, 4, 2),
-                                                    (40, 24, 6, 3)])
-def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows, inflight):
+@pytest.mark.parametrize("W,H,band_rows,inflight,stage_host", [(48, 27, 4, 1, None), (40, 24, 6, 1, None),
+                                                               (48, 27, 4, 2, None), (40, 24, 6, 3, None),
+                                                               (40, 24, 6, 3, True)])
+def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows, inflight, stage_host):
+    """stage_host=True: the host-staged gather bench.py uses for gloo ranks on one GPU."""
     from helpers import params_for
     import frm
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, inflight, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, inflight, q, stage_host)) for r in range(2)]
     for pr in procs:
         pr.start()
     frame, counters, frames = q.get(timeout=180)

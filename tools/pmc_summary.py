@@ -8,7 +8,11 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fractal-ray-marching_amd"))
+from frm import provenance  # noqa: E402
 
 
 KERNEL = "march_persistent"
@@ -59,6 +63,9 @@ def main(d):
         "hbm_write_bytes": c.get("WRITE_SIZE", 0) * 1024,
         "hbm_read_bytes": 2 * c.get("FETCH_SIZE", 0) * 1024,
         "hbm_write_gbps": c.get("WRITE_SIZE", 0) * 1024 / t / 1e9,
+        "dispatches_averaged": len(dur),
+        # the kernel sources these counters were measured on (bench.py cites only a match)
+        "source_sha256": provenance.source_sha256(),
     }
     print(json.dumps(s, indent=1))
     return s
