@@ -13,8 +13,8 @@
 //    finite non-zero operands with a normal quotient it only re-applies the sign).
 //    Zero numerators are handled exactly: 0 / b = +-0 with sign(a) ^ sign(b).
 //  * log2 / exp2: the special-value selects are dead for positive normal finite inputs /
-//    finite exponents, and exp2's clamp cannot change the result for y >= -400 (2^y
-//    then rounds to +0 either way).
+//    finite exponents; the exponent split of log2 and the scaling of exp2 are integer
+//    arithmetic on the encodings where the operand (log2) / result (exp2) is normal.
 #pragma once
 #include "frm_math.h"
 
@@ -66,20 +66,43 @@ __device__ __forceinline__ float div_tame_nz(float a, float b) {
 
 // sincos_ for finite |x| <= 2^22 * pi/2 (the quadrant clamp is a no-op there); negating through
 // the sign bit: (q & 2) ? -v : v == v ^ (bit 1 of q moved to bit 31). Bit-identical.
+// rint(x * 2/pi) by the 1.5 * 2^23 rounding constant: |x * 2/pi| < 2^22, so t = x * 2/pi + K
+// rounds to an integer (to nearest even, as rint does), j = t - K is exact and the low bits
+// of t's encoding are j mod 2^22 (two v_add in place of v_rndne + v_cvt). The odd-quadrant
+// swap is a bit-field select on a sign-extended bit 0 (no compare, no v_cndmask).
+#ifndef FRM_FAST_V1
+__device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) {  // (mask & a) | (~mask & b)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+  return r;
+}
+#endif
 __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
+#ifdef FRM_FAST_V1
   float j = rintf(x * kTwoOverPi);
+  const uint32_t q = (uint32_t)(int)j;
+#else
+  const float tq = x * kTwoOverPi + 0x1.8p23f;
+  const float j = tq - 0x1.8p23f;
+  const uint32_t q = __float_as_uint(tq);
+#endif
   float r = fma_(-j, kHalfPi, x);
   r = fma_(-j, kHalfPiLo, r);
-  const uint32_t q = (uint32_t)(int)j;
   float z = r * r;
   float ps = fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
   float s = fma_(r * z, ps, r);
   float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
                   4.166664568298827e-2f);
   float c = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
+#ifdef FRM_FAST_V1
   const bool odd = (q & 1u) != 0u;
   float sv = odd ? c : s;
   float cv = odd ? s : c;
+#else
+  const uint32_t odd = (uint32_t)((int32_t)(q << 31) >> 31);  // v_bfe_i32 q, 0, 1
+  const float sv = __uint_as_float(bfi_(odd, __float_as_uint(c), __float_as_uint(s)));
+  const float cv = __uint_as_float(bfi_(odd, __float_as_uint(s), __float_as_uint(c)));
+#endif
   *s_out = __uint_as_float(__float_as_uint(sv) ^ ((q << 30) & 0x80000000u));
   *c_out = __uint_as_float(__float_as_uint(cv) ^ (((q + 1u) << 30) & 0x80000000u));
 }
@@ -123,21 +146,58 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
   return copysignf(r, y);
 }
 
+// log_split_ for positive normal finite x by integer arithmetic (the musl logf split):
+// ix = bits(x) - bits(sqrt(1/2)); k = ix >> 23 (arithmetic) is the exponent for a mantissa
+// in [sqrt(1/2), sqrt(2)) and bits(x) - (ix & 0xff800000) that mantissa: the same m and e
+// as frexp + the doubling below sqrt(1/2) (x = m0 * 2^e, m0 in [1/2, 1): m0 >= sqrt(1/2)
+// keeps m0, else 2 m0 with e - 1), without v_frexp, the compare and the selects.
+__device__ __forceinline__ void log_split_normal(float x, float* f_out, float* e_out) {
+#ifdef FRM_FAST_V1
+  log_split_(x, f_out, e_out);
+#else
+  const uint32_t ix = __float_as_uint(x) - 0x3f3504f3u;  // bits of kSqrtHalf
+  *f_out = __uint_as_float(__float_as_uint(x) - (ix & 0xff800000u)) - 1.0f;
+  *e_out = (float)((int32_t)ix >> 23);
+#endif
+}
+
 // log2_ for positive normal finite x.
 __device__ __forceinline__ float log2_tame(float x) {
   float f, fe;
-  log_split_(x, &f, &fe);
+  log_split_normal(x, &f, &fe);
   return fma_(log1p_kernel_(f), kLog2e, fe);
 }
 
-// exp2_ for finite y in [-400, 128].
+// log_ for positive normal finite x (log_posfinite_ with the integer split).
+__device__ __forceinline__ float log_posnormal(float x) {
+  float f, fe;
+  log_split_normal(x, &f, &fe);
+  float l = log1p_kernel_(f);
+  return fma_(fe, 0.693359375f, fma_(fe, -2.12194440e-4f, l));
+}
+
+// exp2_ for finite y whose rint lies in [-125, 127] (y in [-125.5, 127.5)): there the
+// result 2^f * 2^k is a normal number (2^f in [2^-1/2, 2^1/2]), so ldexp is an add of k to
+// the exponent field, and rint(y) comes from the 1.5 * 2^23 rounding constant: the low 9
+// bits of t = y + K's encoding are k mod 512, so (bits(t) << 23) == k << 23 mod 2^32
+// (one v_lshl_add_u32 in place of v_rndne, v_cvt and v_ldexp). The clamp to [-151, 129]
+// cannot fire there.
 __device__ __forceinline__ float exp2_tame(float y) {
+#ifdef FRM_FAST_V1
   float k = rintf(y);
+#else
+  const float t = y + 0x1.8p23f;
+  const float k = t - 0x1.8p23f;
+#endif
   float f = y - k;
   float p = fma_(fma_(fma_(fma_(fma_(1.535336188319500e-4f, f, 1.339887440266574e-3f), f,
                                9.618437357674640e-3f), f, 5.550332471162809e-2f), f,
                      2.402264791363012e-1f), f, 6.931472028550421e-1f);
+#ifdef FRM_FAST_V1
   return ldexpf(fma_(f, p, 1.0f), (int)k);
+#else
+  return __uint_as_float(__float_as_uint(fma_(f, p, 1.0f)) + (__float_as_uint(t) << 23));
+#endif
 }
 
 #endif  // __HIP_DEVICE_COMPILE__

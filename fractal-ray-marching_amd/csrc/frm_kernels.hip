@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256) void eval_math(int fn, const float* a, const f
     case 15: r = acos_dev(x); break;
     case 16: r = atan2_tame(x, y); break;
     case 17: r = log2_tame(x); break;
-    default: r = exp2_tame(x); break;
+    case 18: r = exp2_tame(x); break;
+    default: r = log_posnormal(x); break;
 #else
     default: r = x; break;
 #endif

@@ -185,16 +185,22 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     //    shadow ray) and the record store of a finished pixel are branches.
     const bool cons = pix != kIdle && done;
     bool ev_bail = false;
-    // the distance's log without its special-value selects when no consuming lane has a
-    // magnitude that is 0, negative, infinite or NaN (wave-uniform test; same bits)
+    // the distance's log without its special-value selects (and with the integer exponent
+    // split) when every consuming lane's magnitude is positive, normal and finite
+    // (wave-uniform test; same bits)
     bool plain_log = true;
     if constexpr (FAM == kMandelbulb)
-      plain_log = ballot(cons && !__builtin_amdgcn_classf(mag, 0x180 /* +subnormal, +normal */)) == 0;
+      plain_log = ballot(cons && !__builtin_amdgcn_classf(mag, 0x100 /* +normal */)) == 0;
     if (cons) {
       done = false;
       if constexpr (FAM == kMandelbulb) {
         FRM_SUB_BEGIN();
-        de = plain_log ? mb_distance_posfinite(mag, dr) : mb_distance(mag, dr);
+#if defined(__HIP_DEVICE_COMPILE__)
+        de = plain_log ? mb_distance_posnormal(mag, dr) : mb_distance(mag, dr);
+#else
+        (void)plain_log;
+        de = mb_distance(mag, dr);
+#endif
         pix_cost += body;          // bodies this DE ran (N+1 on a count exit)
         ev_bail = body <= n_iter;  // exit by bailout (incl. before the first body)
         FRM_SUB_END(0);

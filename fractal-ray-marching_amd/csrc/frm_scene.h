@@ -190,6 +190,10 @@ FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 FRM_HD float mb_distance(float r, float dr) { return ((0.5f * log_(r)) * r) / dr; }
 // mb_distance for positive finite r (log_'s special-value selects cannot fire): same bits.
 FRM_HD float mb_distance_posfinite(float r, float dr) { return ((0.5f * log_posfinite_(r)) * r) / dr; }
+#if defined(__HIP_DEVICE_COMPILE__)
+// mb_distance for positive normal finite r (integer exponent split, frm_fast.h): same bits.
+__device__ __forceinline__ float mb_distance_posnormal(float r, float dr) { return ((0.5f * log_posnormal(r)) * r) / dr; }
+#endif
 
 #if defined(__HIPCC__)
 // Lane mask of a per-lane predicate (no int round trip, unlike HIP's __ballot(int)).
@@ -213,10 +217,11 @@ __device__ __forceinline__ bool lane_in(uint64_t mask) {
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Operands of one Mandelbulb body are tame when r = length(z) is in [2^-40, bailout]
+// Operands of one Mandelbulb body are tame when r = length(z) is in [2^-13, bailout]
 // and every component of z is 0 or has magnitude >= 2^-60: then z.z / r and
 // min/max(|x|,|y|) are tame divisions, log2(r) has a positive normal argument and both
-// exp2 arguments ((P-1)*log2 r, P*log2 r with P <= 9) lie in [-400, 128].
+// exp2 arguments ((P-1)*log2 r, P*log2 r with P in [4, 9], log2 r in [-13, log2 100])
+// lie in [-117, 60], where exp2_tame's result is normal.
 // Branch-free: (bits << 1) - 1 drops the sign and maps +-0 to UINT_MAX, so one unsigned
 // min3 + compare tests "0 or |v| >= 2^-60" for the three components at once (NaN
 // components also pass, but then r is NaN and fails r >= 2^-40).
@@ -224,7 +229,11 @@ __device__ __forceinline__ uint32_t comp_key(float v) { return (__float_as_uint(
 __device__ __forceinline__ bool mb_tame(v3 z, float r) {
   constexpr uint32_t kMin = (0x21800000u << 1) - 1u;  // comp_key(0x1p-60f)
   const uint32_t m = min(min(comp_key(z.x), comp_key(z.y)), comp_key(z.z));  // v_min3_u32
+#ifdef FRM_FAST_V1
   return (r >= 0x1p-40f) & (m >= kMin);
+#else
+  return (r >= 0x1p-13f) & (m >= kMin);
+#endif
 }
 
 // mb_body (frm_scene.h) with the tame primitives: the same operations in the same order.

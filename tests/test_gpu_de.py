@@ -82,6 +82,7 @@ def test_mandelbulb_tame_and_exact_paths(gpu_renderer_factory, oracle):
     odd[1::64] = [1e-25, 2e-26, -3e-25]  # |z|^2 < 2^-96
     odd[2::64] = [0.0, 0.0, 1e-13]
     odd[3::64] = [0.0, 0.0, 0.0]
+    odd[4::64] = [1e-5, -2e-5, 3e-5]  # |z| in [2^-40, 2^-13): exact body since exp2_tame's domain
     for iters in (3, 12):
         p = params_for(18, iters, frm.POWER8_TIME, 64, 64)
         with gpu_renderer_factory() as r:
@@ -127,15 +128,23 @@ def _fast_inputs(name, rng):
         edge = np.array([0.0, -0.0, 2.0 ** -60, -(2.0 ** -60), 2.0 ** 40, -(2.0 ** 40), 1.0])
         ey, ex = (g.ravel() for g in np.meshgrid(edge, edge))
         return "atan2", np.concatenate([_tame(rng, n), ey]), np.concatenate([_tame(rng, n), ex])
-    if name == "log2_tame":
-        return "log2", np.concatenate([np.exp2(rng.uniform(-126, 128, n)), [1.0, 2.0 ** -126, 0.7071067]]), None
-    # exp2_tame: finite y in [-400, 128]
-    a = np.concatenate([rng.uniform(-400, 128, n), rng.uniform(-1, 1, 1000), np.arange(-150, 129), [-400.0, 127.999]])
+    if name in ("log2_tame", "log_posnormal"):
+        # positive normal finite x, incl. both sides of every sqrt(1/2) mantissa boundary
+        edge = np.float32(0.70710677).view(np.uint32) + np.arange(-2, 3, dtype=np.int64)
+        edge = np.concatenate([np.ldexp(edge.astype(np.uint32).view(np.float32).astype(np.float64), e)
+                               for e in range(-125, 128, 7)])
+        a = np.concatenate([np.exp2(rng.uniform(-126, 128, n)), edge,
+                            [1.0, 2.0 ** -126, 0.7071067, np.finfo(np.float32).max, 2.0, 0.5]])
+        return ("log2" if name == "log2_tame" else "log"), a, None
+    # exp2_tame: finite y with rint(y) in [-125, 127]: [-125.5, 127.5), the half-way points
+    # rounding to even at both ends included
+    a = np.concatenate([rng.uniform(-125.5, 127.49, n), rng.uniform(-1, 1, 1000), np.arange(-125, 128),
+                        np.arange(-125, 127) + 0.5, [-125.5, 127.499]])
     return "exp2", a, None
 
 
 FAST = ["sqrt_nosmall", "div_tame", "div_tame_nz", "sin_small", "cos_small", "acos_dev", "atan2_tame",
-        "log2_tame", "exp2_tame"]
+        "log2_tame", "exp2_tame", "log_posnormal"]
 
 
 @pytest.mark.parametrize("name", FAST)
