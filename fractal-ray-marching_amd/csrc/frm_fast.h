@@ -70,13 +70,11 @@ __device__ __forceinline__ float div_tame_nz(float a, float b) {
 // rounds to an integer (to nearest even, as rint does), j = t - K is exact and the low bits
 // of t's encoding are j mod 2^22 (two v_add in place of v_rndne + v_cvt). The odd-quadrant
 // swap is a bit-field select on a sign-extended bit 0 (no compare, no v_cndmask).
-#ifndef FRM_FAST_V1
 __device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) {  // (mask & a) | (~mask & b)
   uint32_t r;
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
   return r;
 }
-#endif
 __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
 #ifdef FRM_FAST_V1
   float j = rintf(x * kTwoOverPi);
@@ -118,7 +116,15 @@ __device__ __forceinline__ float acos_dev(float t) {
   float p = fma_(fma_(fma_(fma_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
                       7.4953002686e-2f), z, 1.6666752422e-1f);
   float s = fma_(w * z, p, w);
+#ifndef FRM_ACOS_SELECT
+  // rb is used only for |t| > 1/2 (t != 0): t > 0 is t's sign bit, and (t > 0 ? 2s : pi - 2s)
+  // == fma(2s, t < 0 ? -1 : 1, t < 0 ? pi : 0), one rounding either way
+  const uint32_t tb = __float_as_uint(t);
+  float rb = fma_(2.0f * s, __uint_as_float(bfi_(0x80000000u, tb, 0x3f800000u)),
+                  __uint_as_float((uint32_t)((int32_t)tb >> 31) & __float_as_uint(kPi)));
+#else
   float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
+#endif
   float rs = kHalfPi - copysignf(s, t);
   return big ? rb : rs;
 }
@@ -141,8 +147,19 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
                           0.10678940285181907f), s, -0.14214209135918496f), s,
                 0.1999413720560495f), s, -0.3333316696611865f);
   float r = fma_(a * s, q, a);
+#ifndef FRM_ATAN_SELECT
+  // the octant fix-ups without compares: (c ? h - r : r) == fma(r, c ? -1 : 1, c ? h : 0), one
+  // rounding either way (r >= +0). c = sign bit of ax - ay (exact difference: negative iff
+  // ay > ax, +0 when equal) and of x + 0 (-0 + 0 = +0: negative iff x < 0).
+  const uint32_t c1 = __float_as_uint(ax - ay), c2 = __float_as_uint(x + 0.0f);
+  r = fma_(r, __uint_as_float(bfi_(0x80000000u, c1, 0x3f800000u)),
+           __uint_as_float((uint32_t)((int32_t)c1 >> 31) & __float_as_uint(kHalfPi)));
+  r = fma_(r, __uint_as_float(bfi_(0x80000000u, c2, 0x3f800000u)),
+           __uint_as_float((uint32_t)((int32_t)c2 >> 31) & __float_as_uint(kPi)));
+#else
   r = (ay > ax) ? kHalfPi - r : r;
   r = (x < 0.0f) ? kPi - r : r;
+#endif
   return copysignf(r, y);
 }
 

@@ -460,8 +460,8 @@ static vec3 calculate_normal(const om_frame* F, vec3 p, om_counts* C) {
 #define INFO_SHADOW_FIRST_NONPOS 8u
 #define INFO_ZERO_NORMAL 16u
 
-/* fragment_main; returns linear colour, fills counters and a per-pixel info word */
-static vec3 fragment(const om_frame* F, uint32_t x, uint32_t y, om_counts* C, uint32_t* info) {
+/* Camera ray of pixel (x, y): fragment.wgsl:329-330 with vertex.wgsl's pixel centre. */
+static vec3 camera_dir(const om_frame* F, uint32_t x, uint32_t y) {
   const float CAMERA_DIRECTION_Z = (float)(1.0 / atan(90.0 * 3.141592653589793238 / 180.0));
   float sx = (float)(2u * x + 1u) / (float)F->width - 1.0f;
   float sy = 1.0f - (float)(2u * y + 1u) / (float)F->height;
@@ -471,29 +471,57 @@ static vec3 fragment(const om_frame* F, uint32_t x, uint32_t y, om_counts* C, ui
     const float* c = &F->M[4 * j];
     dir[j] = fmaf(0.0f, c[3], fmaf(d0.z, c[2], fmaf(d0.y, c[1], d0.x * c[0])));
   }
-  vec3 camera_direction = V(dir[0], dir[1], dir[2]);
+  return V(dir[0], dir[1], dir[2]);
+}
+
+static const vec3 TO_SUN = {0.666666686534881592f, 0.333333343267440796f, -0.666666686534881592f};
+
+/* Shading of a hit, fragment.wgsl:336-346, from the march's geometric results: the object
+ * colour, primary steps, normal and the shadow march's distance and closeness. The only
+ * builtins are the two pows (specular, ambient occlusion), in the frame's math mode. */
+static vec3 shade_hit(const om_frame* F, vec3 camera_direction, vec3 color, uint32_t steps, vec3 n,
+                      float sun_distance, float sun_closeness) {
+  vec3 halfway = vnormalize(vadd(vneg(camera_direction), TO_SUN));
+  float specular = b_pow(F->mode, wmax(vdot(halfway, n), 0.0f), 16.0f);
+  float ao = b_pow(F->mode, 1.0f - (float)steps / (float)F->max_steps, 100.0f);
+  color = vscale(color, wmix(0.2f, 1.0f, ao));
+  float shadow = ((sun_distance < 0.0f ? 1.0f : 0.0f) * 32.0f) * sun_closeness;
+  color = vscale(color, wmix(0.7f, 1.0f, wclamp(shadow, 0.0f, 1.0f)));
+  float add = ((0.15f * shadow) * specular) * 1.0f;
+  return vadd(color, V(add, add, add));
+}
+
+/* Per-pixel trace of the geometric inputs of the shading (parity classification, P1):
+ * hit, primary steps, normal xyz, sun hit, sun closeness, object colour xyz. */
+#define OM_TRACE_FLOATS 10
+
+/* fragment_main; returns linear colour, fills counters, a per-pixel info word and (if
+ * trace) the OM_TRACE_FLOATS geometric shading inputs */
+static vec3 fragment(const om_frame* F, uint32_t x, uint32_t y, om_counts* C, uint32_t* info, float* trace) {
+  vec3 camera_direction = camera_dir(F, x, y);
   march_result obj = march(F, F->origin, camera_direction, &C->primary, C);
   vec3 color = obj.color;
   uint32_t inf = obj.steps << 8;
+  if (trace) {
+    memset(trace, 0, OM_TRACE_FLOATS * sizeof(float));
+    trace[1] = (float)obj.steps;
+  }
   if (obj.distance >= 0.0f) {
     inf |= INFO_HIT;
     C->hits++;
     vec3 n = calculate_normal(F, obj.position, C);
     if (n.x != n.x) inf |= INFO_ZERO_NORMAL;
-    const vec3 to_sun = V(0.666666686534881592f, 0.333333343267440796f, -0.666666686534881592f);
-    vec3 halfway = vnormalize(vadd(vneg(camera_direction), to_sun));
-    float specular = b_pow(F->mode, wmax(vdot(halfway, n), 0.0f), 16.0f);
     vec3 start = V(fmaf(n.x * 2.0f, MIN_DISTANCE, obj.position.x), fmaf(n.y * 2.0f, MIN_DISTANCE, obj.position.y),
                    fmaf(n.z * 2.0f, MIN_DISTANCE, obj.position.z));
-    march_result sun = march(F, start, to_sun, &C->shadow, C);
+    march_result sun = march(F, start, TO_SUN, &C->shadow, C);
     if (sun.distance >= 0.0f) inf |= INFO_SUN_HIT;
     if (sun.closeness != sun.closeness || sun.closeness == -INFINITY) inf |= INFO_SHADOW_FIRST_NONPOS;
-    float ao = b_pow(F->mode, 1.0f - (float)obj.steps / (float)F->max_steps, 100.0f);
-    color = vscale(color, wmix(0.2f, 1.0f, ao));
-    float shadow = ((sun.distance < 0.0f ? 1.0f : 0.0f) * 32.0f) * sun.closeness;
-    color = vscale(color, wmix(0.7f, 1.0f, wclamp(shadow, 0.0f, 1.0f)));
-    float add = ((0.15f * shadow) * specular) * 1.0f;
-    color = vadd(color, V(add, add, add));
+    if (trace) {
+      const float t[OM_TRACE_FLOATS] = {1.0f, (float)obj.steps, n.x, n.y, n.z, sun.distance >= 0.0f ? 1.0f : 0.0f,
+                                        sun.closeness, color.x, color.y, color.z};
+      memcpy(trace, t, sizeof(t));
+    }
+    color = shade_hit(F, camera_direction, color, obj.steps, n, sun.distance, sun.closeness);
     if (color.x != color.x || color.y != color.y || color.z != color.z) inf |= INFO_NAN;
   }
   *info = inf;
@@ -534,6 +562,7 @@ typedef struct {
   uint8_t* rgba;
   float* linear;
   uint32_t* info;
+  float* trace;
   uint32_t next; /* atomic row cursor (rayon-like dynamic schedule) */
   pthread_mutex_t mu;
   om_counts total;
@@ -550,9 +579,9 @@ static void* worker(void* arg) {
     uint32_t y = J->rows ? J->rows[r] : r;
     for (uint32_t x = 0; x < W; ++x) {
       uint32_t inf;
-      vec3 c = fragment(J->F, x, y, &C, &inf);
+      const size_t i = (size_t)r * W + x;
+      vec3 c = fragment(J->F, x, y, &C, &inf, J->trace ? J->trace + OM_TRACE_FLOATS * i : NULL);
       C.pixels++;
-      size_t i = (size_t)r * W + x;
       uint8_t* px = J->rgba + 4 * i;
       px[0] = encode(c.x);
       px[1] = encode(c.y);
@@ -597,9 +626,10 @@ static void frame_from_params(om_frame* F, const uint8_t* params96, uint32_t wid
 /* Render `nrows` rows (rows[i], or 0..nrows-1 when rows == NULL) of a width x height frame.
  * counters (8 x u64, same order as libfrm's device counters): pixels, hits, primary
  * steps, shadow steps, normal evals, Mandelbulb bodies, bailouts, 0. */
-int om_render(const uint8_t* params96, uint32_t width, uint32_t height, uint32_t max_steps, uint32_t flags,
-              int mode, const uint32_t* rows, uint32_t nrows, int threads, uint8_t* out_rgba,
-              uint64_t* counters, float* out_linear, uint32_t* out_info) {
+int om_render_trace(const uint8_t* params96, uint32_t width, uint32_t height, uint32_t max_steps,
+                    uint32_t flags, int mode, const uint32_t* rows, uint32_t nrows, int threads,
+                    uint8_t* out_rgba, uint64_t* counters, float* out_linear, uint32_t* out_info,
+                    float* out_trace) {
   if (!params96 || !out_rgba || width == 0 || height == 0 || threads < 1) return 1;
   for (uint32_t i = 0; rows && i < nrows; ++i)
     if (rows[i] >= height) return 1;
@@ -614,6 +644,7 @@ int om_render(const uint8_t* params96, uint32_t width, uint32_t height, uint32_t
   J.rgba = out_rgba;
   J.linear = out_linear;
   J.info = out_info;
+  J.trace = out_trace;
   pthread_mutex_init(&J.mu, NULL);
   pthread_t* tid = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
   if (!tid) return 2;
@@ -634,6 +665,38 @@ int om_render(const uint8_t* params96, uint32_t width, uint32_t height, uint32_t
     counters[5] = J.total.bodies;
     counters[6] = J.total.bailouts;
     counters[7] = 0;
+  }
+  return 0;
+}
+
+int om_render(const uint8_t* params96, uint32_t width, uint32_t height, uint32_t max_steps, uint32_t flags,
+              int mode, const uint32_t* rows, uint32_t nrows, int threads, uint8_t* out_rgba,
+              uint64_t* counters, float* out_linear, uint32_t* out_info) {
+  return om_render_trace(params96, width, height, max_steps, flags, mode, rows, nrows, threads, out_rgba, counters,
+                         out_linear, out_info, NULL);
+}
+
+/* Re-shade n pixels (x, y interleaved in xy) from traces (OM_TRACE_FLOATS each, as
+ * om_render_trace writes them) with the shading of `mode`, and encode them: the colour the
+ * pixel would have with those geometric inputs. */
+int om_shade_trace(const uint8_t* params96, uint32_t width, uint32_t height, uint32_t max_steps, uint32_t flags,
+                   int mode, const uint32_t* xy, uint32_t n, const float* trace, uint8_t* out_rgba) {
+  if (!params96 || !xy || !trace || !out_rgba || width == 0 || height == 0) return 1;
+  pthread_once(&g_srgb_once, srgb_init);
+  om_frame F;
+  frame_from_params(&F, params96, width, height, max_steps, flags, mode);
+  for (uint32_t i = 0; i < n; ++i) {
+    const float* t = trace + (size_t)OM_TRACE_FLOATS * i;
+    if (xy[2 * i] >= width || xy[2 * i + 1] >= height) return 1;
+    vec3 c = V(0.0f, 0.0f, 0.0f);
+    if (t[0] != 0.0f)
+      c = shade_hit(&F, camera_dir(&F, xy[2 * i], xy[2 * i + 1]), V(t[7], t[8], t[9]), (uint32_t)t[1],
+                    V(t[2], t[3], t[4]), t[5] != 0.0f ? 0.0f : -INF_1E20, t[6]);
+    uint8_t* px = out_rgba + 4 * (size_t)i;
+    px[0] = encode(c.x);
+    px[1] = encode(c.y);
+    px[2] = encode(c.z);
+    px[3] = 255;
   }
   return 0;
 }

@@ -21,6 +21,9 @@ INFO_NAN = 4
 INFO_SHADOW_FIRST_NONPOS = 8
 INFO_ZERO_NORMAL = 16
 
+# per-pixel trace (render(trace=True)): the geometric inputs of the shading
+TRACE_FIELDS = ("hit", "steps", "nx", "ny", "nz", "sun_hit", "sun_closeness", "cr", "cg", "cb")
+
 MATH_FN = {"sin": 0, "cos": 1, "acos": 2, "atan2": 3, "log": 4, "log2": 5, "exp2": 6,
            "pow": 7, "sqrt": 8, "div": 9}
 
@@ -42,6 +45,11 @@ def load():
                                   ctypes.c_uint32, ctypes.c_int, u32p, ctypes.c_uint32, ctypes.c_int,
                                   u8p, u64p, f32p, u32p]
         lib.om_render.restype = ctypes.c_int
+        lib.om_render_trace.argtypes = lib.om_render.argtypes + [f32p]
+        lib.om_render_trace.restype = ctypes.c_int
+        lib.om_shade_trace.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_int, u32p, ctypes.c_uint32, f32p, u8p]
+        lib.om_shade_trace.restype = ctypes.c_int
         lib.om_scene_de.argtypes = [u8p, ctypes.c_uint32, ctypes.c_int, f32p, ctypes.c_uint32, f32p,
                                     f32p, u64p]
         lib.om_scene_de.restype = ctypes.c_int
@@ -69,8 +77,9 @@ def _params_buf(params):
 
 
 def render(params, width, height, max_steps, flags=0, mode=MODE_FRM, rows=None, threads=None,
-           linear=False, info=False):
-    """Render rows (default all) -> dict(rgba=[n,W,4] u8, counters=[8] u64, ...)."""
+           linear=False, info=False, trace=False):
+    """Render rows (default all) -> dict(rgba=[n,W,4] u8, counters=[8] u64, ...); info: the
+    per-pixel INFO_* bits | primary steps << 8; trace: [n,W,len(TRACE_FIELDS)] f32."""
     lib = load()
     pb = _params_buf(params)
     if rows is None:
@@ -83,9 +92,11 @@ def render(params, width, height, max_steps, flags=0, mode=MODE_FRM, rows=None, 
     counters = np.zeros(8, dtype=np.uint64)
     lin = np.zeros((nrows, width, 3), dtype=np.float32) if linear else None
     inf = np.zeros((nrows, width), dtype=np.uint32) if info else None
-    rc = lib.om_render(pb.ctypes.data, width, height, max_steps, flags, mode, rows_ptr, nrows, threads,
-                       rgba.ctypes.data, counters.ctypes.data,
-                       lin.ctypes.data if linear else None, inf.ctypes.data if info else None)
+    tr = np.zeros((nrows, width, len(TRACE_FIELDS)), dtype=np.float32) if trace else None
+    rc = lib.om_render_trace(pb.ctypes.data, width, height, max_steps, flags, mode, rows_ptr, nrows, threads,
+                             rgba.ctypes.data, counters.ctypes.data,
+                             lin.ctypes.data if linear else None, inf.ctypes.data if info else None,
+                             tr.ctypes.data if trace else None)
     if rc != 0:
         raise RuntimeError(f"om_render failed ({rc})")
     out = {"rgba": rgba, "counters": counters}
@@ -93,6 +104,22 @@ def render(params, width, height, max_steps, flags=0, mode=MODE_FRM, rows=None, 
         out["linear"] = lin
     if info:
         out["info"] = inf
+    if trace:
+        out["trace"] = tr
+    return out
+
+
+def shade_trace(params, width, height, max_steps, xs, ys, trace, flags=0, mode=MODE_FRM):
+    """RGBA8 of pixels (xs[i], ys[i]) shaded (fragment.wgsl:336-346, builtins of `mode`) from
+    the given traces ([n, len(TRACE_FIELDS)]) instead of their own march results."""
+    lib = load()
+    xy = np.ascontiguousarray(np.stack([xs, ys], axis=-1), dtype=np.uint32)
+    tr = np.ascontiguousarray(trace, dtype=np.float32).reshape(-1, len(TRACE_FIELDS))
+    out = np.zeros((len(tr), 4), dtype=np.uint8)
+    rc = lib.om_shade_trace(_params_buf(params).ctypes.data, width, height, max_steps, flags, mode,
+                            xy.ctypes.data, len(tr), tr.ctypes.data, out.ctypes.data)
+    if rc != 0:
+        raise ValueError("om_shade_trace")
     return out
 
 
