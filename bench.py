@@ -35,15 +35,6 @@ import subprocess
 import sys
 import time
 
-# Frames in flight overlap only on distinct hardware queues. HIP maps streams onto at most
-# GPU_MAX_HW_QUEUES queues per process (4, HIP's default, which the GPU boxes export), shared
-# by the null stream, torch's streams, libfrm's and RCCL's; a render stream that shares a
-# queue with another waits behind its packets (measured: with 4 queues the second render
-# stream lands on the timing stream's queue and two frames in flight never overlap). Raised
-# before torch initialises HIP.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "fractal-ray-marching_amd")
 for _p in (ROOT, PKG):
@@ -76,6 +67,12 @@ def parse():
                     help="frames in flight per GPU (frm_config.frames_in_flight): frame k+1 renders "
                     "while frame k's longest pixels finish; 1 = one frame at a time; 0 = 3 for a rank's "
                     "bands of a split frame and frames below 4 M pixels, else 2 (measured best, DESIGN.md)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0: raise to 16 if lower). Frames in flight "
+                    "overlap only on distinct hardware queues: HIP maps streams onto at most that many "
+                    "queues per process (4, HIP's default), shared by the null stream, torch's, libfrm's "
+                    "and RCCL's; with 4 the second render stream lands on the timing stream's queue and "
+                    "two frames in flight never overlap (DESIGN.md section 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
@@ -213,6 +210,11 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args)
+    # before torch initialises HIP
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
+    elif int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
     import torch
     import torch.distributed as dist
 
@@ -375,7 +377,8 @@ def main():
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
-                "pose": args.pose, "frames_in_flight": inflight, "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
+                "pose": args.pose, "frames_in_flight": inflight,
+                "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + "
                                 f"{'RCCL' if backend == 'nccl' else backend + ' (host-staged)'} gather" if split > 1 else

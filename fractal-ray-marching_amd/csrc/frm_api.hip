@@ -37,7 +37,7 @@ struct Slot {
   hipStream_t last_stream = nullptr;  // stream of the slot's last launch
   uint8_t* fb = nullptr;         // frm_render's framebuffer for this slot
   unsigned int* queue = nullptr;
-  ShadeRecord* records = nullptr;  // persistent kernel scratch, grown on demand
+  uint8_t* records = nullptr;  // persistent kernel scratch (ShadeGeom[cap] then ShadeTail[cap]), grown on demand
   size_t records_cap = 0;
   // pixel scheduling state (frm_sched.hip), sched_cap entries each: 0..cap-1, the fetch
   // order, the cost keys the slot's last launch recorded per pixel and the sort's key output
@@ -48,6 +48,8 @@ struct Slot {
   size_t sched_cap = 0, sched_temp_bytes = 0;
   uint64_t sched_key = 0;  // geometry the recorded keys belong to
   bool sched_history = false;
+  uint32_t sched_w = 0, sched_h = 0;  // frame size of the recorded keys when they cover a whole frame
+  bool sched_whole = false;
 };
 
 struct frm_ctx {
@@ -195,18 +197,28 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       if (sl.records) FRM_HIP(ctx, hipFree(sl.records));
       sl.records = nullptr;
       sl.records_cap = 0;
-      FRM_HIP(ctx, hipMalloc(&sl.records, need * sizeof(ShadeRecord)));
+      FRM_HIP(ctx, hipMalloc(&sl.records, need * kRecordBytes));
       sl.records_cap = need;
     }
-    a.records = sl.records;
+    a.geom = reinterpret_cast<ShadeGeom*>(sl.records);
+    a.tails = reinterpret_cast<ShadeTail*>(sl.records + sl.records_cap * sizeof(ShadeGeom));
     // pixel scheduling: fetch this launch's pixels by the cost the slot recorded last time
     // for the same geometry (most expensive first)
     const uint32_t npix = a.npix;
+    const uint64_t key = ((uint64_t)a.f.width << 40) ^ ((uint64_t)a.g.local_rows << 20) ^
+                         ((uint64_t)a.g.band_rows << 8) ^ ((uint64_t)a.g.first_band << 4) ^ a.g.band_stride ^
+                         ((uint64_t)a.f.height << 52);
+    // a whole frame (not a rank's bands): its keys can seed a resized whole frame's order
+    const bool whole = a.g.first_band == 0 && a.g.band_stride == 1 && npix == a.f.width * a.f.height;
+    const bool same = sl.sched_history && key == sl.sched_key;
+    const bool rescale = !same && sl.sched_history && sl.sched_whole && whole;
     if (npix > sl.sched_cap) {
       int rc = wait_slot(ctx, sl);
       if (rc) return rc;
-      for (void* b : {(void*)sl.sched_iota, (void*)sl.sched_order, (void*)sl.sched_keys, sl.sched_temp})
+      uint8_t* old_keys = sl.sched_keys;  // kept until a resize has resampled it
+      for (void* b : {(void*)sl.sched_iota, (void*)sl.sched_order, sl.sched_temp})
         if (b) FRM_HIP(ctx, hipFree(b));
+      if (!rescale && old_keys) FRM_HIP(ctx, hipFree(old_keys));
       sl.sched_iota = sl.sched_order = nullptr;
       sl.sched_keys = nullptr;
       sl.sched_temp = nullptr;
@@ -218,18 +230,27 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       FRM_HIP(ctx, hipMalloc(&sl.sched_temp, sl.sched_temp_bytes ? sl.sched_temp_bytes : 16));
       FRM_HIP(ctx, fill_iota(sl.sched_iota, npix, s));
       sl.sched_cap = npix;
-      sl.sched_history = false;
+      if (rescale) {
+        FRM_HIP(ctx, rescale_keys(old_keys, sl.sched_w, sl.sched_h, sl.sched_keys, a.f.width, a.f.height, s));
+        FRM_HIP(ctx, hipStreamSynchronize(s));  // the old map is read before it is freed
+        FRM_HIP(ctx, hipFree(old_keys));
+      }
+    } else if (rescale) {
+      // resample into the sort's output half, then back (the map is read and written)
+      uint8_t* tmp = sl.sched_keys + sl.sched_cap;
+      FRM_HIP(ctx, rescale_keys(sl.sched_keys, sl.sched_w, sl.sched_h, tmp, a.f.width, a.f.height, s));
+      FRM_HIP(ctx, hipMemcpyAsync(sl.sched_keys, tmp, npix, hipMemcpyDeviceToDevice, s));
     }
-    const uint64_t key = ((uint64_t)a.f.width << 40) ^ ((uint64_t)a.g.local_rows << 20) ^
-                         ((uint64_t)a.g.band_rows << 8) ^ ((uint64_t)a.g.first_band << 4) ^ a.g.band_stride ^
-                         ((uint64_t)a.f.height << 52);
-    const bool history = sl.sched_history && key == sl.sched_key;
+    const bool history = same || rescale;
     FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
                                  sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
     a.pixel_order = sl.sched_order;
     a.pixel_key = sl.sched_keys;
     sl.sched_key = key;
     sl.sched_history = true;
+    sl.sched_whole = whole;
+    sl.sched_w = a.f.width;
+    sl.sched_h = a.f.height;
     a.debug = (unsigned long long*)(sl.queue + 8);  // bytes 32..71 of the queue block
     FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, sizeof(unsigned int), s));
 #ifdef FRM_STAMPS
@@ -273,6 +294,9 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   if (config->frames_in_flight > FRM_MAX_FRAMES_IN_FLIGHT)
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.frames_in_flight %u above %u", config->frames_in_flight,
                 FRM_MAX_FRAMES_IN_FLIGHT);
+  if (config->max_steps > FRM_MAX_STEPS_LIMIT)
+    return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.max_steps %u above %u", config->max_steps,
+                FRM_MAX_STEPS_LIMIT);
   const uint32_t kernels = FRM_FLAG_SIMPLE_KERNEL | FRM_FLAG_PERSISTENT_KERNEL;
   if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE)) || (config->flags & kernels) == kernels)
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.flags 0x%x: unknown flag or both kernel flags",
@@ -370,9 +394,6 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
 
 int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters) {
   if (!ctx || !parameters) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/parameters is NULL");
-  if (parameters->num_iterations > FRM_MAX_NUM_ITERATIONS)
-    return fail(ctx, FRM_ERR_UNSUPPORTED, "num_iterations %u above FRM_MAX_NUM_ITERATIONS (%u)",
-                parameters->num_iterations, FRM_MAX_NUM_ITERATIONS);
   ctx->params = *parameters;
   compute_scene_uniforms(ctx->params, ctx->flags, &ctx->scene);
   ctx->has_params = true;

@@ -100,7 +100,11 @@ void compute_scene_uniforms(const frm_parameters& p, uint32_t flags, SceneUnifor
     case 12: set_menger(u, (float)(1.0 / 3.0), animate_between(t, 3.0f, 5.0f)); break;
     case 13: set_menger(u, (float)(1.0 / 4.0), animate_between(t, 2.0f, 4.0f)); break;
     case 14: set_menger(u, (float)(1.0 / 6.0), animate_between(t, 1.2f, 3.0f)); break;
-    case 15: set_sierpinski(u, p.num_iterations); break;
+    case 15:
+      set_sierpinski(u, p.num_iterations);
+      // `for (var i = i32(N) - 1; i >= 0; i--)` (fragment.wgsl:181): no fold for N >= 2^31
+      if ((int32_t)p.num_iterations < 0) u->n = 0;
+      break;
     case 16: set_koch(u, p.num_iterations, (float)sqrt(3.0)); break;
     case 17: set_koch(u, p.num_iterations, animate_between(t, (float)sqrt(3.0), 4.0f)); break;
     case 18:

@@ -15,15 +15,24 @@ struct BandGeometry {
   uint32_t band_rows, first_band, band_stride, local_rows;
 };
 
-// Per-pixel result of the persistent march kernel, consumed by the shading pass (32 B).
-struct ShadeRecord {
-  float t, nx, ny, nz;      // primary hit distance, surface normal (written at the last tap)
-  float closeness;          // shadow march closeness
-  uint32_t psteps;          // primary march steps (ambient occlusion)
-  uint32_t flags;           // kRecHit | kRecSunMiss; 0 = primary miss
-  uint32_t key;             // scheduling cost key (frm_sched.hip); shade_pass copies it out
+// Per-pixel results of the persistent march kernel, consumed by the shading pass: two arrays
+// indexed by local pixel.
+//  * ShadeTail (8 B, every pixel, one store when its march ends): the shadow march's
+//    closeness and one word packing the primary steps (bits 0-21), kRecHit, kRecSunMiss and
+//    the scheduling cost key (bits 24-31, frm_sched.hip; shade_pass copies it out).
+//  * ShadeGeom (16 B, hit pixels only, one store at the last normal tap): primary hit
+//    distance and surface normal. Misses never touch it.
+struct ShadeTail {
+  float closeness;
+  uint32_t word;
 };
-constexpr uint32_t kRecHit = 1u, kRecSunMiss = 2u;
+struct ShadeGeom {
+  float t, nx, ny, nz;
+};
+constexpr uint32_t kRecStepsMask = (1u << 22) - 1u;  // primary steps < 2^22 (FRM_MAX_STEPS_LIMIT)
+constexpr uint32_t kRecHit = 1u << 22, kRecSunMiss = 1u << 23;
+constexpr uint32_t kRecKeyShift = 24;
+constexpr size_t kRecordBytes = sizeof(ShadeTail) + sizeof(ShadeGeom);  // scratch per local pixel
 
 struct KernelArgs {
   FrameUniforms f;
@@ -32,7 +41,8 @@ struct KernelArgs {
   uint32_t* out;                  // packed RGBA8 words, local row-major, pitch = width
   unsigned long long* counters;   // FRM_NUM_COUNTERS, accumulated
   unsigned int* queue;            // persistent kernel: work-queue head (zeroed per launch)
-  ShadeRecord* records;           // persistent kernel: local_rows * width records
+  ShadeGeom* geom;                // persistent kernel: local_rows * width hit records
+  ShadeTail* tails;               // persistent kernel: local_rows * width march-end records
   uint32_t npix;                  // persistent kernel: pixels of the launch (= fetch positions)
   uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
   unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
@@ -77,6 +87,9 @@ hipError_t schedule_pixels(uint32_t npix, bool has_history, const uint8_t* key, 
                            const uint32_t* iota, uint32_t* order, void* temp, size_t temp_bytes,
                            hipStream_t stream);
 hipError_t fill_iota(uint32_t* out, uint32_t n, hipStream_t stream);
+// Whole-frame key map sw x sh -> dw x dh, nearest neighbour (history across a resize).
+hipError_t rescale_keys(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
+                        hipStream_t stream);
 size_t schedule_temp_bytes(uint32_t npix);
 hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
                              hipStream_t stream);

@@ -67,7 +67,8 @@ __global__ __launch_bounds__(256) void render_simple(KernelArgs a) {
 // pixels from a global queue (one atomic per chunk) in the order frm_sched.hip chose
 // (most expensive pixels first), and computes the chunk's 64 camera rays in one coherent
 // pass into LDS. Instead of shading at low lane occupancy, a finished
-// pixel stores a 32-byte ShadeRecord; shade_pass then shades and sRGB-packs all pixels
+// pixel stores an 8-byte ShadeTail (+ a 16-byte ShadeGeom for a hit, at its last normal
+// tap); shade_pass then shades and sRGB-packs all pixels
 // coherently. Per-pixel arithmetic is the same operation sequence as shade_pixel<>, so
 // the bytes are identical to render_simple and the oracle.
 constexpr uint32_t kIdle = 0xFFFFFFFFu;
@@ -105,7 +106,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   const uint64_t lane_bit = 1ull << lane;
   const uint32_t total = a.npix;
   const uint32_t n_iter = iterations<ITERS>(su.n);
-  ShadeRecord* __restrict__ rec = a.records;
+  ShadeGeom* __restrict__ geom = a.geom;
+  ShadeTail* __restrict__ tails = a.tails;
 
   // wave-uniform state: current chunk of 64 fetched pixels, how many were handed out
   uint32_t slots_used = kChunk;
@@ -195,7 +197,10 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       done = false;
       if constexpr (FAM == kMandelbulb) {
         FRM_SUB_BEGIN();
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)  // measurement build: one path for every lane
+        (void)plain_log;
+        de = mb_distance_posnormal(mag, dr);
+#elif defined(__HIP_DEVICE_COMPILE__)
         de = plain_log ? mb_distance_posnormal(mag, dr) : mb_distance(mag, dr);
 #else
         (void)plain_log;
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       FRM_SUB_BEGIN();
       const v3 n = normalize(nsum);
       const v3 hp = ray_at(o, t, d);
-      *reinterpret_cast<float4*>(&rec[pix].t) = make_float4(t, n.x, n.y, n.z);
+      *reinterpret_cast<float4*>(&geom[pix]) = make_float4(t, n.x, n.y, n.z);
       o = shadow_origin(hp, n);
       d = to_sun();
       t = 0.f;
@@ -248,8 +253,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     if (fin) {  // primary miss (flags 0: BACKGROUND_COLOR) or end of the shadow march
       FRM_SUB_BEGIN();
       const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
-      *reinterpret_cast<uint4*>(&rec[pix].closeness) =
-          make_uint4(__float_as_uint(closeness), psteps, flags, cost_key(pix_cost));
+      *reinterpret_cast<uint2*>(&tails[pix]) =
+          make_uint2(__float_as_uint(closeness), psteps | flags | ((uint32_t)cost_key(pix_cost) << kRecKeyShift));
       pix = kIdle;
       FRM_SUB_END(3);
     }
@@ -400,17 +405,17 @@ __global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
   const uint32_t lr = idx / width, x = idx - lr * width;
   const uint32_t y = band_row_to_global(a.g, lr);
   if (y >= a.f.height) return;
-  const uint4 r1 = *reinterpret_cast<const uint4*>(&a.records[idx].closeness);
-  if (a.pixel_key) a.pixel_key[idx] = (uint8_t)r1.w;  // coalesced, for the next frame's order
+  const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[idx]);
+  if (a.pixel_key) a.pixel_key[idx] = (uint8_t)(r1.y >> kRecKeyShift);  // coalesced, for the next frame's order
   uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
-  if (r1.z & kRecHit) {
-    const float4 r0 = *reinterpret_cast<const float4*>(&a.records[idx].t);
+  if (r1.y & kRecHit) {
+    const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[idx]);
     const v3 dir = camera_ray(a.f, x, y);
     const v3 hp = ray_at(a.f.origin, r0.x, dir);
     const v3 n = mk(r0.y, r0.z, r0.w);
     float spec;
-    v3 color = shade_hit_pre(a.f, scene_color<FAM>(hp), dir, n, r1.y, &spec);
-    color = shade_hit_post(color, spec, (r1.z & kRecSunMiss) ? -kInfinity : 0.0f, __uint_as_float(r1.x));
+    v3 color = shade_hit_pre(a.f, scene_color<FAM>(hp), dir, n, r1.y & kRecStepsMask, &spec);
+    color = shade_hit_post(color, spec, (r1.y & kRecSunMiss) ? -kInfinity : 0.0f, __uint_as_float(r1.x));
     word = pack_rgba(color, table);
   }
   a.out[idx] = word;

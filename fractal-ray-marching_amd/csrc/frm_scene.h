@@ -25,7 +25,8 @@ namespace frm {
 
 // ITERS template flag: false <=> num_iterations == 0. The fractal loops of every family
 // are compiled twice: without a loop (ITERS = false) and with the trip count asserted
-// to be >= 1 (ITERS = true), so no device code ever evaluates the uniform guard
+// to be >= 1 (ITERS = true; any u32 above that, as the reference's Parameters allows),
+// so no device code ever evaluates the uniform guard
 // "num_iterations > 0" inside the divergent march loop. ROCm 7.2's AMDGPU backend
 // miscompiles that guard (it is rematerialised as a lane mask under the loop's exec
 // mask and reused after the loop with a different exec mask), which re-entered the
@@ -33,7 +34,7 @@ namespace frm {
 template <bool ITERS>
 FRM_HD uint32_t iterations(uint32_t n) {
   if (!ITERS) return 0u;
-  FRM_ASSUME(n >= 1u && n <= 4096u);
+  FRM_ASSUME(n >= 1u);
   return n;
 }
 
@@ -138,8 +139,9 @@ FRM_HD float de_menger(const SceneUniforms& u, v3 p) {
   return d;
 }
 
-// sierpinski_tetrahedron(position), fragment.wgsl:164-188. The loop runs i = N-1 .. 0
-// (num_iterations <= FRM_MAX_NUM_ITERATIONS < 2^31, so i32(N) - 1 >= -1).
+// sierpinski_tetrahedron(position), fragment.wgsl:164-188. The loop runs i = N-1 .. 0; for
+// N >= 2^31, i32(N) - 1 < 0 and WGSL's loop runs zero times: the host then passes n = 0
+// (compute_scene_uniforms).
 template <bool ITERS>
 FRM_HD float de_sierpinski(const SceneUniforms& u, v3 p) {
   const uint32_t n = iterations<ITERS>(u.n);
@@ -186,13 +188,73 @@ FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
   sincos_(phi * P, &sp, &cp);
   z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
 }
+#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
+// MEASUREMENT BUILD ONLY (-DFRM_HW_MATH, tools/gpu_hw_math.sh; never the product): the
+// Mandelbulb body and distance with gfx950's hardware transcendentals, as a Vulkan driver
+// lowers fragment.wgsl's builtins: log2/exp2 -> v_log_f32/v_exp_f32, sin/cos -> v_sin/v_cos
+// (argument in revolutions), sqrt -> v_sqrt_f32, a / b -> a * v_rcp_f32(b); acos and atan2
+// keep their polynomials on those primitives. Not bit-exact with the oracle by design: DESIGN
+// §5 prices exact math against it.
+__device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float hw_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ void hw_sincos(float x, float* s, float* c) {
+  const float rev = x * 0.15915494309189535f;
+  *s = __builtin_amdgcn_sinf(rev);
+  *c = __builtin_amdgcn_cosf(rev);
+}
+__device__ __forceinline__ float hw_acos(float t) {
+  float a = fabsf(t);
+  bool big = a > 0.5f;
+  float zb = 0.5f * (1.0f - a);
+  float z = big ? zb : a * a;
+  float w = big ? hw_sqrt(zb) : a;
+  float p = fma_(fma_(fma_(fma_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
+                      7.4953002686e-2f), z, 1.6666752422e-1f);
+  float s = fma_(w * z, p, w);
+  float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
+  return big ? rb : kHalfPi - copysignf(s, t);
+}
+__device__ __forceinline__ float hw_atan2(float y, float x) {
+  float ax = fabsf(x), ay = fabsf(y);
+  float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  float a = mx == 0.0f ? 0.0f : hw_div(mn, mx);
+  float s = a * a;
+  float q = fma_(fma_(fma_(fma_(fma_(fma_(fma_(0.002974590389872539f, s, -0.016581183968493302f), s,
+                                      0.04355353931255974f), s, -0.07580578130128461f), s,
+                          0.10678940285181907f), s, -0.14214209135918496f), s,
+                0.1999413720560495f), s, -0.3333316696611865f);
+  float r = fma_(a * s, q, a);
+  r = (ay > ax) ? kHalfPi - r : r;
+  r = (x < 0.0f) ? kPi - r : r;
+  return copysignf(r, y);
+}
+__device__ __forceinline__ void mb_body_hw(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+  float theta = hw_acos(hw_div(z.z, r));
+  float phi = hw_atan2(z.y, z.x);
+  float l2 = __builtin_amdgcn_logf(r);
+  dr = fma_(__builtin_amdgcn_exp2f(Pm1 * l2) * P, dr, 1.0f);
+  float er = __builtin_amdgcn_exp2f(P * l2);
+  float st, ct, sp, cp;
+  hw_sincos(theta * P, &st, &ct);
+  hw_sincos(phi * P, &sp, &cp);
+  z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
+}
+#endif
+
 // distance = 0.5 * log(magnitude) * magnitude / magnitude_derivative, fragment.wgsl:269
 FRM_HD float mb_distance(float r, float dr) { return ((0.5f * log_(r)) * r) / dr; }
 // mb_distance for positive finite r (log_'s special-value selects cannot fire): same bits.
 FRM_HD float mb_distance_posfinite(float r, float dr) { return ((0.5f * log_posfinite_(r)) * r) / dr; }
 #if defined(__HIP_DEVICE_COMPILE__)
 // mb_distance for positive normal finite r (integer exponent split, frm_fast.h): same bits.
-__device__ __forceinline__ float mb_distance_posnormal(float r, float dr) { return ((0.5f * log_posnormal(r)) * r) / dr; }
+__device__ __forceinline__ float mb_distance_posnormal(float r, float dr) {
+#ifdef FRM_HW_MATH
+  return hw_div((0.5f * (__builtin_amdgcn_logf(r) * 0.6931471805599453f)) * r, dr);
+#else
+  return ((0.5f * log_posnormal(r)) * r) / dr;
+#endif
+}
 #endif
 
 #if defined(__HIPCC__)
@@ -259,9 +321,14 @@ __device__ __forceinline__ bool length_small(v3 a) {
 
 #endif
 
+
 // One Mandelbulb body; on the GPU the wave takes the tame fast path (frm_fast.h) when all
 // its active lanes have tame operands. Bit-identical to mb_body either way.
 FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
+  mb_body_hw(u, c, r, z, dr);
+  return;
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   if (ballot(!mb_tame(z, r)) == 0) {
     mb_body_tame(u, c, r, z, dr);
@@ -272,6 +339,9 @@ FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
 }
 // length(z) for the Mandelbulb magnitude; fast sqrt unless a lane has 0 < |z|^2 < 2^-96.
 FRM_HD float mb_length(v3 z) {
+#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
+  return hw_sqrt(dot(z, z));
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   if (ballot(length_small(z)) == 0) return length_nosmall(z);
 #endif

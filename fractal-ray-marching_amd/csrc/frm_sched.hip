@@ -28,6 +28,25 @@ size_t schedule_temp_bytes(uint32_t npix) {
   return bytes;
 }
 
+// Nearest-neighbour resample of a whole-frame key map (sw x sh, row-major) to dw x dh: the
+// history a resized frame starts from (the cost of a pixel is a smooth-ish function of its
+// screen position, so the old frame's keys order the new frame's first launch).
+__global__ void rescale_keys_kernel(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw,
+                                    uint32_t dh) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= dw * dh) return;
+  const uint32_t y = i / dw, x = i - y * dw;
+  const uint32_t sy = (uint32_t)(((uint64_t)y * sh) / dh), sx = (uint32_t)(((uint64_t)x * sw) / dw);
+  dst[i] = src[(size_t)sy * sw + sx];
+}
+
+hipError_t rescale_keys(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
+                        hipStream_t stream) {
+  const uint32_t n = dw * dh;
+  hipLaunchKernelGGL(rescale_keys_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, src, sw, sh, dst, dw, dh);
+  return hipGetLastError();
+}
+
 hipError_t fill_iota(uint32_t* out, uint32_t n, hipStream_t stream) {
   hipLaunchKernelGGL(iota_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, out, n);
   return hipGetLastError();

@@ -24,7 +24,8 @@ FRM_ERR_COMPILE = 8
 FRM_NUM_SCENES = 19
 FRM_MAX_FRAMES_IN_FLIGHT = 8
 FRM_DEFAULT_MAX_STEPS = 5000
-FRM_MAX_NUM_ITERATIONS = 4096
+FRM_MAX_STEPS_LIMIT = 4194303
+FRM_MAX_NUM_ITERATIONS = 0xFFFFFFFF
 FRM_NUM_COUNTERS = 8
 FRM_FLAG_SCENE_SPHERE = 0x1
 FRM_FLAG_SIMPLE_KERNEL = 0x2

@@ -45,7 +45,7 @@ enum {
   FRM_ERR_OUT_OF_MEMORY = 4,    /* device allocation failed                           */
   FRM_ERR_NOT_READY = 5,        /* frm_render before frm_resize / frm_set_parameters  */
   FRM_ERR_BUFFER_TOO_SMALL = 6, /* destination smaller than the frame or band set      */
-  FRM_ERR_UNSUPPORTED = 7,      /* e.g. num_iterations above FRM_MAX_NUM_ITERATIONS    */
+  FRM_ERR_UNSUPPORTED = 7,      /* an operation this build does not support            */
   FRM_ERR_COMPILE = 8           /* frm_reload: the sources failed to compile (log in last_error) */
 };
 
@@ -79,7 +79,8 @@ _Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
 
 #define FRM_NUM_SCENES 19u            /* parameters.rs:35 (NUM_SCENES)                 */
 #define FRM_DEFAULT_MAX_STEPS 5000u   /* fragment.wgsl:4 (MAX_ITERATIONS)              */
-#define FRM_MAX_NUM_ITERATIONS 4096u  /* guard: fractal loops are O(num_iterations)    */
+#define FRM_MAX_NUM_ITERATIONS 0xffffffffu /* any u32, as parameters.rs:31-33 saturates;
+                                          a frame's fractal loops are O(num_iterations) */
 #define FRM_MAX_DIMENSION 32768u      /* width/height limit per frame                  */
 
 /* config flags */
@@ -100,8 +101,9 @@ _Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
 typedef struct frm_config {
   int32_t device;     /* HIP device ordinal (replaces the wgpu adapter request,
                          persistent_graphics.rs:43-50)                                 */
-  uint32_t max_steps; /* march() step cap; 0 = FRM_DEFAULT_MAX_STEPS. It also feeds the
-                         ambient-occlusion term (fragment.wgsl:289,342)               */
+  uint32_t max_steps; /* march() step cap; 0 = FRM_DEFAULT_MAX_STEPS, at most
+                         FRM_MAX_STEPS_LIMIT. It also feeds the ambient-occlusion term
+                         (fragment.wgsl:289,342)                                         */
   uint32_t flags;     /* FRM_FLAG_*                                                    */
   uint32_t frames_in_flight; /* frames a context may have in flight on the GPU at once,
                          1..FRM_MAX_FRAMES_IN_FLIGHT (0 = 1). Each render launch (frm_render,
@@ -113,6 +115,9 @@ typedef struct frm_config {
 } frm_config;
 
 #define FRM_MAX_FRAMES_IN_FLIGHT 8u
+/* largest frm_config.max_steps: the persistent kernel packs a pixel's primary step count
+   into 22 bits of its 8-byte record (the reference's MAX_ITERATIONS is 5000) */
+#define FRM_MAX_STEPS_LIMIT 4194303u
 
 /* Work counters of one render (exact; equal to the CPU oracle's counts). */
 typedef struct frm_stats {

@@ -71,6 +71,9 @@ def test_errors_are_codes_not_crashes(frm_lib):
     ctx = ctypes.c_void_p()
     bad = _lib.FrmConfig(0, 0, 0, _lib.FRM_MAX_FRAMES_IN_FLIGHT + 1)  # frames_in_flight above the cap
     assert L.frm_create(ctypes.byref(ctx), ctypes.byref(bad)) == _lib.FRM_ERR_INVALID_ARGUMENT
+    bad = _lib.FrmConfig(0, _lib.FRM_MAX_STEPS_LIMIT + 1, 0, 1)  # max_steps above the record's 22 bits
+    assert L.frm_create(ctypes.byref(ctx), ctypes.byref(bad)) == _lib.FRM_ERR_INVALID_ARGUMENT
+    assert b"max_steps" in L.frm_last_error(None)
 
 
 def test_create_without_gpu_reports_no_device(frm_lib):

@@ -1,0 +1,42 @@
+"""Resizing keeps the pixel-scheduling history: the first frame of a new whole-frame size
+fetches its pixels in the order of the previous size's cost keys, resampled (frm_sched.hip
+rescale_keys), instead of row-major. Order never changes bytes: every frame of a resize
+sequence (up, down, odd sizes; one and two frames in flight) equals the oracle's. Also:
+num_iterations above the old 4096 cap renders the reference's semantics (Sierpinski's
+i32(N) loop runs no fold for N >= 2^31)."""
+import numpy as np
+import pytest
+
+import frm
+from helpers import params_for
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("inflight", [1, 2])
+def test_resize_sequence_bit_exact(frm_lib, oracle, inflight):
+    sizes = [(96, 54), (160, 90), (64, 36), (130, 9), (160, 90)]
+    with frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL, frames_in_flight=inflight) as r:
+        for w, h in sizes:
+            p = params_for(18, 12, frm.POWER8_TIME, w, h)
+            r.resize(w, h)
+            r.update_parameters_buffer(p)
+            ref = oracle.render(p, w, h, 256)
+            for k in range(inflight + 1):  # the first frame(s) of the size, then a scheduled one
+                st = r.render(stats=True)
+                img = r.read_frame()
+                assert np.array_equal(img, ref["rgba"]), f"{w}x{h} frame {k}"
+                assert st["march_steps"] == int(ref["counters"][2] + ref["counters"][3])
+
+
+@pytest.mark.parametrize("scene,iters", [(15, 2 ** 31 + 5), (15, 0xFFFFFFFF), (18, 5000), (0, 4100)])
+def test_num_iterations_above_old_cap(frm_lib, oracle, scene, iters):
+    w, h = 32, 18
+    p = params_for(scene, iters, frm.POWER8_TIME, w, h)
+    with frm.Renderer(device=0, max_steps=64) as r:
+        r.resize(w, h)
+        r.update_parameters_buffer(p)
+        r.render(stats=False)
+        img = r.read_frame()
+    ref = oracle.render(p, w, h, 64)
+    assert np.array_equal(img, ref["rgba"])

@@ -2,11 +2,17 @@
 on whole frames. Scenes without transcendentals in their DE are byte-identical; the
 chaotic Mandelbulb differs on a small, measured fraction of pixels (a 1-ulp change in a
 builtin flips hit points after 12 power-8 iterations). Tolerances below are the measured
-values with margin; DESIGN.md §Parity records them."""
+values with margin; DESIGN.md §Parity records them. The classified tests assign every
+pixel that differs by more than one code to a geometric class and require the shading and
+encode path to agree within one code between the modes everywhere (tests/p1_classify.py),
+at BASELINE sizes too (the 4K headline and C2, whole frames)."""
+import os
+
 import numpy as np
 import pytest
 
 import frm
+import p1_classify
 from helpers import params_for
 
 
@@ -32,3 +38,28 @@ def test_mandelbulb_within_measured_tolerance(oracle, pose, bound):
     # aggregate work differs by well under 1%
     sa, sb = int(a["counters"][2] + a["counters"][3]), int(b["counters"][2] + b["counters"][3])
     assert abs(sa - sb) / sa < 0.01
+
+
+def _check_classified(r):
+    assert r["unexplained"] == 0, r
+    assert r["shading_mode_gt1_anywhere"] == 0, r
+    assert sum(r["classes"].values()) == r["differ_gt1"], r
+
+
+@pytest.mark.parametrize("pose", ["P0", "P1", "P2"])
+def test_mandelbulb_differences_classified(oracle, pose):
+    r = p1_classify.classify(oracle, params_for(18, 12, frm.POWER8_TIME, 320, 180, pose=pose), 320, 180, 256)
+    _check_classified(r)
+    assert r["differ_gt1_frac"] < 0.06
+
+
+@pytest.mark.parametrize("name", ["HEADLINE", "C2"])
+def test_mandelbulb_differences_classified_full_size(oracle, name):
+    """The bench's frames at BASELINE size: every >1-code pixel of the whole 3840x2160
+    headline and 1920x1080 C2 frame (pose P1) is in a geometric class, none unexplained
+    (about 3 CPU-minutes for the headline on 8 cores)."""
+    w = frm.WORKLOADS[name]
+    r = p1_classify.classify(oracle, frm.make_parameters(w, pose="P1"), w.width, w.height, w.max_steps,
+                             threads=os.cpu_count())
+    _check_classified(r)
+    assert r["differ_gt1_frac"] < 0.06
