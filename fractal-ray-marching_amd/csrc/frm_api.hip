@@ -20,7 +20,7 @@ using namespace frm;
 
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
-static constexpr uint32_t kDefaultServiceMin = 20;  // swept 16..36 on MI355X (round 1): flat 16-24
+static constexpr uint32_t kDefaultServiceMin = 24;  // swept 16..36 on MI355X (round 1: 20); round-2 kernel: headline 16/20/24/28 = 11.43/11.36/11.18/11.24 ms, C2 flat
 // Kernel choice without a FRM_FLAG_*_KERNEL flag: below one resident persistent grid
 // (6 blocks of 256 lanes per CU for the Mandelbulb) a launch has fewer pixels than lanes,
 // and the persistent kernel's fixed costs (pixel sort, grid, separate shading pass) outweigh

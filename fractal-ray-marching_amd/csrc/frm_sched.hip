@@ -28,16 +28,26 @@ size_t schedule_temp_bytes(uint32_t npix) {
   return bytes;
 }
 
-// Nearest-neighbour resample of a whole-frame key map (sw x sh, row-major) to dw x dh: the
-// history a resized frame starts from (the cost of a pixel is a smooth-ish function of its
-// screen position, so the old frame's keys order the new frame's first launch).
+// Resample of a whole-frame key map (sw x sh, row-major) to dw x dh: the history a resized
+// frame starts from. A new pixel takes the largest key of the source pixels its footprint
+// covers, widened by one source pixel on every side (at most 8 x 8 of them). Costs are not
+// smooth on a fractal (grazing rays along silhouettes are the expensive ones, and they move
+// between resolutions), and for longest-first list scheduling an over-estimate only starts a
+// cheap pixel early while an under-estimate leaves an expensive one for the tail.
 __global__ void rescale_keys_kernel(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw,
                                     uint32_t dh) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= dw * dh) return;
   const uint32_t y = i / dw, x = i - y * dw;
-  const uint32_t sy = (uint32_t)(((uint64_t)y * sh) / dh), sx = (uint32_t)(((uint64_t)x * sw) / dw);
-  dst[i] = src[(size_t)sy * sw + sx];
+  const uint32_t x0 = (uint32_t)(((uint64_t)x * sw) / dw), y0 = (uint32_t)(((uint64_t)y * sh) / dh);
+  const uint32_t x1 = (uint32_t)(((uint64_t)(x + 1) * sw + dw - 1) / dw);
+  const uint32_t y1 = (uint32_t)(((uint64_t)(y + 1) * sh + dh - 1) / dh);
+  const uint32_t xa = x0 > 0 ? x0 - 1 : 0, ya = y0 > 0 ? y0 - 1 : 0;
+  const uint32_t xb = min(min(x1 + 1, sw), xa + 8), yb = min(min(y1 + 1, sh), ya + 8);
+  uint32_t k = 0;
+  for (uint32_t sy = ya; sy < yb; ++sy)
+    for (uint32_t sx = xa; sx < xb; ++sx) k = max(k, (uint32_t)src[(size_t)sy * sw + sx]);
+  dst[i] = (uint8_t)k;
 }
 
 hipError_t rescale_keys(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,

@@ -31,7 +31,7 @@ def cumask_stream(dev):
     return torch.cuda.ExternalStream(st.value, device=dev)
 
 
-def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=False, cumask=False):
+def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=False, cumask=False, gather=False):
     """mode 'slots': one context with frames_in_flight = F; 'contexts': F contexts."""
     w = frm.WORKLOADS[workload]
     p = frm.make_parameters(w, pose="P1")
@@ -56,6 +56,13 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
         ss.append(cumask_stream(dev) if cumask else torch.cuda.Stream(device=dev))
         bufs.append(torch.zeros(rows * w.width * 4, dtype=torch.uint8, device=dev))
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    # gather: rank 0's extra work per frame of a real P-way run, on its render stream after its
+    # bands: P - 1 rank buffers arriving (device-to-device copies of its own buffer stand in
+    # for RCCL's receives over xGMI) and frm_unshuffle_bands into the row-major frame
+    gbufs = frames_out = None
+    if gather and ranks > 1:
+        gbufs = [torch.zeros(ranks * bufs[0].numel(), dtype=torch.uint8, device=dev) for _ in range(inflight)]
+        frames_out = [torch.zeros(w.width * w.height * 4, dtype=torch.uint8, device=dev) for _ in range(inflight)]
 
     def go(n):
         for k in range(n):
@@ -64,6 +71,14 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
                 torch.cuda.Event(enable_timing=True).record(ss[i])
             rs[i].render_bands(bufs[i].data_ptr(), bufs[i].numel(), br, rank, ranks, ss[i].cuda_stream,
                                counters.data_ptr())
+            if gbufs is not None:
+                with torch.cuda.stream(ss[i]):
+                    nb = bufs[i].numel()
+                    gbufs[i][:nb].copy_(bufs[i])
+                    for q in range(1, ranks):
+                        gbufs[i][q * nb:(q + 1) * nb].copy_(bufs[i], non_blocking=True)
+                rs[i].unshuffle_bands(gbufs[i].data_ptr(), nb, frames_out[i].data_ptr(), frames_out[i].numel(),
+                                      br, ranks, ss[i].cuda_stream)
             if events:
                 torch.cuda.Event(enable_timing=True).record(ss[i])
 
@@ -78,6 +93,7 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
     for r in set(rs):
         r.close()
     return {"workload": workload, "ranks": ranks, "rank": rank, "inflight": inflight, "mode": mode, "events": events, "cumask": cumask,
+            "gather": bool(gbufs is not None),
             "ms_per_frame": dt / frames * 1e3, "gsteps": st["march_steps"] / dt / 1e9}
 
 
@@ -92,6 +108,7 @@ def main():
     ap.add_argument("--cumask", default="0")
     ap.add_argument("--repeat", type=int, default=1)
     ap.add_argument("--rank-ids", default="0", help="ranks whose share to time ('all' = every rank)")
+    ap.add_argument("--gather", default="0", help="1: rank 0 also receives and unshuffles (see run())")
     args = ap.parse_args()
     for wl in args.workloads.split(","):
         for P in [int(x) for x in args.ranks.split(",")]:
@@ -101,8 +118,11 @@ def main():
                         for cm in [bool(int(x)) for x in args.cumask.split(",")]:
                             ids = range(P) if args.rank_ids == "all" else [int(x) for x in args.rank_ids.split(",") if int(x) < P]
                             for rk in ids:
-                                for _ in range(args.repeat):
-                                    print(json.dumps(run(wl, P, rk, F, args.frames, 2, m, ev, cm)), flush=True)
+                                for g in [bool(int(x)) for x in args.gather.split(",")]:
+                                    if g and rk != 0:
+                                        continue
+                                    for _ in range(args.repeat):
+                                        print(json.dumps(run(wl, P, rk, F, args.frames, 2, m, ev, cm, g)), flush=True)
 
 
 if __name__ == "__main__":
