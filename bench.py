@@ -3,7 +3,9 @@
 
 Workload (BASELINE.json metric): 3840x2160 Mandelbulb (scene 18 at power 8), 12 DE
 iterations, 256 march steps, fixed camera pose P1; one "step" = one whole frame of the
-hot path (fragment_main for every pixel) with inputs resident on the GPU.
+hot path (fragment_main for every pixel) with inputs resident on the GPU. Frames are
+rendered several per launch (--batch; frm_render_bands_batch): every frame is computed in
+full, the frames' pixels share one work queue so a launch's tail is paid once per batch.
 
 N GPUs (one process each): launched by torch.distributed.run (the driver's multi-GPU runs),
 or, when no launcher set WORLD_SIZE, bench.py starts `torch.distributed.run` itself as a child
@@ -64,15 +66,20 @@ def parse():
                     "rank 0 (strong scaling); 'frames' = alternate-frame rendering, each rank renders "
                     "whole frames of an orbit fly-through (no data-path collective, weak scaling)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU (frm_config.frames_in_flight): frame k+1 renders "
-                    "while frame k's longest pixels finish; 1 = one frame at a time; 0 = 3 for a rank's "
-                    "bands of a split frame and frames below 4 M pixels, else 2 (measured best, DESIGN.md)")
+                    help="launches in flight per GPU (frm_config.frames_in_flight): launch k+1 renders "
+                    "while launch k's longest pixels finish; 0 = measured best (DESIGN.md): with several "
+                    "frames per launch 2 for a rank's bands and frames below 4 M pixels, else 1; one frame "
+                    "per launch 3 / 2")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for this process (0: raise to 16 if lower). Frames in flight "
                     "overlap only on distinct hardware queues: HIP maps streams onto at most that many "
                     "queues per process (4, HIP's default), shared by the null stream, torch's, libfrm's "
                     "and RCCL's; with 4 the second render stream lands on the timing stream's queue and "
                     "two frames in flight never overlap (DESIGN.md section 5)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per launch (frm_render_bands_batch: the frames' pixels share one work "
+                    "queue, so a launch's tail is paid once per batch); 0 = auto (DESIGN.md section 7); "
+                    "animated workloads (a new time every frame) always 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
@@ -260,8 +267,22 @@ def main():
     # frames in flight: a frame's costliest pixels set its tail, which weighs more the fewer
     # pixels a launch has (measured: 4K/8K whole frames best at 2, 1080p and a rank's share
     # of a split frame at 3)
-    inflight = args.inflight or (3 if split > 1 or local_pixels < 4_000_000 else 2)
+    # frames per launch: the frames' pixels share one work queue, so a launch's tail (its
+    # costliest pixels' sequential marches) is paid once per batch (measured, DESIGN.md section 7:
+    # 8-way rank share 1.67 ms/frame at 1 frame per launch and 3 in flight -> 1.38-1.44 at 8 per
+    # launch and 2 in flight; whole 4K frame 11.20 -> 10.89 ms at 4 per launch; 1080p 3.12 ->
+    # 2.81). Animated workloads change the scene every frame and render one frame per launch.
+    batch = 1 if w.animated else max(1, min(args.batch or (8 if split > 1 else 4), frm.FRM_MAX_BATCH))
+    if args.inflight:
+        inflight = args.inflight
+    elif batch > 1:
+        inflight = 2 if split > 1 or local_pixels < 4_000_000 else 1
+    else:
+        inflight = 3 if split > 1 or local_pixels < 4_000_000 else 2
     inflight = max(1, min(inflight, frm.FRM_MAX_FRAMES_IN_FLIGHT))
+    # whole batches: timed and warmup frame counts rounded up to multiples of the batch
+    args.steps = -(-args.steps // batch) * batch
+    args.warmup = -(-args.warmup // batch) * batch
     r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=inflight)
     r.resize(w.width, w.height)
     r.update_parameters_buffer(params)
@@ -286,17 +307,21 @@ def main():
         if timing["on"]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(s)
-        r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
+        if batch > 1:  # one launch, `batch` frames (same scene and camera here), frame b at b * tf.nbytes
+            r.render_bands_batch([params] * batch, buf.data_ptr(), tf.nbytes, br, first, stride, s.cuda_stream,
+                                 counters.data_ptr())
+        else:
+            r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
         if ev is not None:
             ev[1].record(s)
             kev.append(ev)
 
-    def unshuffle(gathered, frame, slot):
-        r.unshuffle_bands(gathered.data_ptr(), gathered.numel() // world, frame.data_ptr(), frame.numel(),
+    def unshuffle(gathered, rank_stride, frame, slot):
+        r.unshuffle_bands(gathered.data_ptr(), rank_stride, frame.data_ptr(), frame.numel(),
                           band_rows, world, streams[slot].cuda_stream)
 
     tf = RowTiledFrame(w.width, w.height, 0 if split == 1 else rank, split, band_rows, dev, render_bands, unshuffle,
-                       inflight=inflight, streams=streams)
+                       inflight=inflight, streams=streams, batch=batch)
 
     # Animated workloads (C5): every frame advances time by 1/60 s through the reference's
     # Timing::update (frm_timing_update), as the reference's frame loop does
@@ -377,7 +402,7 @@ def main():
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
-                "pose": args.pose, "frames_in_flight": inflight,
+                "pose": args.pose, "frames_in_flight": inflight, "frames_per_launch": batch,
                 "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
                 "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + "

@@ -142,6 +142,9 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.counters = counters;
   a.npix = band_valid_rows(ctx->height, a.g) * ctx->width;
   a.service_min = ctx->service_min;
+  a.batch = 1;
+  a.rec_stride = local_rows * ctx->width;
+  a.out_stride = local_rows * ctx->width;
   return a;
 }
 
@@ -190,7 +193,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   const KernelKind kind = kernel_for(ctx, a.npix);
   a.queue = sl.queue;
   if (kind == kKernelPersistent) {
-    const size_t need = (size_t)a.g.local_rows * a.f.width;
+    const size_t need = (size_t)a.g.local_rows * a.f.width * a.batch;
     if (need > sl.records_cap) {  // grows outside the steady state (first frame of a size)
       int rc = wait_slot(ctx, sl);
       if (rc) return rc;
@@ -522,6 +525,63 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   unsigned long long* counters = dev_counters ? (unsigned long long*)dev_counters : ctx->counters;
   KernelArgs a = make_args(ctx, dev_dst, counters, band_rows, first_band, band_stride, rows);
+  return launch(ctx, a, s);
+}
+
+int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* params, uint8_t* dev_dst,
+                           size_t frame_stride_bytes, uint32_t band_rows, uint32_t first_band, uint32_t band_stride,
+                           void* stream, uint64_t* dev_counters) {
+  if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!params || !dev_dst || count == 0 || count > FRM_MAX_BATCH || band_rows == 0 || band_stride == 0)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "invalid batch (count %u, at most %u) or band geometry", count,
+                FRM_MAX_BATCH);
+  const uint32_t rows = band_local_rows(ctx->height, band_rows, first_band, band_stride);
+  const size_t need = (size_t)rows * ctx->width * 4u;
+  if (frame_stride_bytes < need || frame_stride_bytes % 4u)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "frame stride %zu: below a frame's %zu bytes or not a multiple of 4",
+                frame_stride_bytes, need);
+  if ((uint64_t)rows * ctx->width * count >= 0xFFFFFFFFull)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "batch of %u frames of %u x %u local pixels too large", count,
+                ctx->width, rows);
+  // frames of one launch may differ in camera only: same scene uniforms (scene, iterations,
+  // time-derived constants) and aspect
+  SceneUniforms s0;
+  compute_scene_uniforms(params[0], ctx->flags, &s0);
+  for (uint32_t k = 1; k < count; ++k) {
+    SceneUniforms sk;
+    compute_scene_uniforms(params[k], ctx->flags, &sk);
+    if (memcmp(&s0, &sk, sizeof(s0)) != 0 || params[k].aspect_scale[0] != params[0].aspect_scale[0] ||
+        params[k].aspect_scale[1] != params[0].aspect_scale[1])
+      return fail(ctx, FRM_ERR_INVALID_ARGUMENT,
+                  "batch frame %u differs from frame 0 in more than the camera (scene, iterations, time, aspect)", k);
+  }
+  ctx->params = params[count - 1];  // the context's parameters: the batch's last frame
+  ctx->scene = s0;
+  ctx->has_params = true;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  unsigned long long* counters = dev_counters ? (unsigned long long*)dev_counters : ctx->counters;
+  KernelArgs a = make_args(ctx, dev_dst, counters, band_rows, first_band, band_stride, rows);
+  FrameUniforms fk;
+  if (count == 1 || kernel_for(ctx, a.npix) == kKernelSimple || ctx->reloaded) {
+    // one launch per frame (the simple kernel has no queue to share; runtime-reloaded
+    // modules carry the single-frame kernels only)
+    for (uint32_t k = 0; k < count; ++k) {
+      compute_frame_uniforms(params[k], ctx->width, ctx->height, ctx->max_steps, &a.f);
+      a.out = (uint32_t*)(dev_dst + (size_t)k * frame_stride_bytes);
+      int rc = launch(ctx, a, s);
+      if (rc) return rc;
+    }
+    return FRM_OK;
+  }
+  a.batch = count;
+  a.out_stride = (uint32_t)(frame_stride_bytes / 4u);
+  for (uint32_t k = 0; k < count; ++k) {
+    compute_frame_uniforms(params[k], ctx->width, ctx->height, ctx->max_steps, &fk);
+    memcpy(a.cams[k].row, fk.row, sizeof(fk.row));
+    a.cams[k].origin = fk.origin;
+  }
   return launch(ctx, a, s);
 }
 

@@ -9,6 +9,8 @@
 #include "frm_uniforms.h"
 
 namespace frm {
+constexpr uint32_t kMaxBatch = 8;  // FRM_MAX_BATCH: frames per multi-frame launch
+
 // Row-band geometry of one launch: local row lr lives in band (lr / band_rows) of this
 // launch; that band is global band first_band + (lr / band_rows) * band_stride.
 struct BandGeometry {
@@ -48,6 +50,15 @@ struct KernelArgs {
   unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
   const uint32_t* pixel_order;    // persistent kernel: local pixel index at each fetch position
   uint8_t* pixel_key;             // persistent kernel: cost key per local pixel (out)
+  // Multi-frame launch (frm_render_bands_batch): `batch` frames of the same scene share one
+  // work queue; queue chunk c (64 positions) holds pixel_order[(c / batch) * 64 + 0..63] of
+  // frame c % batch (each frame's pixels heaviest first, frames interleaved chunk by chunk).
+  // Frame k's records start at k * rec_stride, its output at out + k * out_stride, its
+  // camera is cams[k]. batch = 1: f.row / f.origin.
+  uint32_t batch;
+  uint32_t rec_stride;            // records per frame
+  uint32_t out_stride;            // packed RGBA8 words per frame
+  FrameCamera cams[kMaxBatch];
 };
 
 #ifndef FRM_MARCH_BLOCK

@@ -131,17 +131,21 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   if (const int v = blocks_override()) bpc = v;
   // every wave starts with one chunk of 64 pixels; never launch more waves than chunks
   uint32_t blocks = (uint32_t)(bpc * cu_count);
-  const uint32_t max_blocks = ((args.npix + kChunk - 1u) / kChunk + kMarchWaves - 1u) / kMarchWaves;
+  const uint32_t positions = args.batch > 1 ? args.batch * ((args.npix + kChunk - 1u) / kChunk) * kChunk : args.npix;
+  const uint32_t max_blocks = ((positions + kChunk - 1u) / kChunk + kMarchWaves - 1u) / kMarchWaves;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) blocks = 1;
   const uint32_t pixels = args.g.local_rows * args.f.width;
   if (rk) {
     hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(kMarchBlock), stream, args);
     if (e != hipSuccess) return e;
-    return module_launch(rk->shade[FAM], dim3((pixels + 255u) / 256u), dim3(256), stream, args);
+    return module_launch(rk->shade[FAM], dim3((pixels + 255u) / 256u, args.batch), dim3(256), stream, args);
   }
-  hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
-  hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u), dim3(256), 0, stream, args);
+  if (args.batch > 1)
+    hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+  else
+    hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+  hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u, args.batch), dim3(256), 0, stream, args);
   return hipGetLastError();
 }
 

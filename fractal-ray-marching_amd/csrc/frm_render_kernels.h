@@ -93,18 +93,25 @@ constexpr uint32_t kWaveDebugSlots = 16384u;
 __device__ unsigned long long g_wave_debug[16u * kWaveDebugSlots];
 #endif
 
-template <uint32_t FAM, bool ITERS>
+// MULTI: a multi-frame launch (frm_render_bands_batch, a.batch > 1), a separate instantiation.
+// Queue chunk c (64 fetch positions) is chunk c / batch of frame c % batch: the frames'
+// pixels interleave chunk by chunk, each frame's longest first, and a chunk's frame (camera)
+// is wave-uniform.
+template <uint32_t FAM, bool ITERS, bool MULTI = false>
 #ifndef FRM_MARCH_WAVES_PER_SIMD
 #define FRM_MARCH_WAVES_PER_SIMD 1
 #endif
 __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
-  __shared__ float4 chunk_rays[kMarchWaves][kChunk];  // per wave: camera ray xyz + local pixel index bits
+  __shared__ float4 chunk_rays[kMarchWaves][kChunk];  // per wave: camera ray xyz + record index bits
 
   const FrameUniforms& f = a.f;
   const SceneUniforms& su = a.s;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t lane_bit = 1ull << lane;
-  const uint32_t total = a.npix;
+  constexpr bool multi = MULTI;
+  // fetch positions (host: < 2^32 - 1); a multi-frame launch pads each frame to whole chunks
+  const uint32_t total = multi ? a.batch * ((a.npix + kChunk - 1u) / kChunk) * kChunk : a.npix;
+  uint32_t chunk_frame = 0;  // wave-uniform: the frame of the wave's current chunk
   const uint32_t n_iter = iterations<ITERS>(su.n);
   ShadeGeom* __restrict__ geom = a.geom;
   ShadeTail* __restrict__ tails = a.tails;
@@ -283,10 +290,21 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           // frame's cost keys, frm_sched.hip), row-major without history
           uint32_t p = kIdle;
           v3 ray = mk(0.f, 0.f, 0.f);
-          if (base + lane < total) {
-            p = a.pixel_order[base + lane];
-            const uint32_t lr = p / f.width, x = p - lr * f.width;
-            ray = camera_ray(f, x, band_row_to_global(a.g, lr));
+          uint32_t pos0 = base, lim = total;
+          if constexpr (multi) {
+            const uint32_t c = base / kChunk;
+            chunk_frame = uniform(c % a.batch);
+            pos0 = (c / a.batch) * kChunk;
+            lim = a.npix;
+          }
+          if (pos0 + lane < lim) {
+            const uint32_t lp = a.pixel_order[pos0 + lane];
+            const uint32_t lr = lp / f.width, x = lp - lr * f.width, y = band_row_to_global(a.g, lr);
+            if constexpr (multi)
+              ray = camera_ray_rows(f, a.cams[chunk_frame].row, x, y);
+            else
+              ray = camera_ray(f, x, y);
+            p = chunk_frame * a.rec_stride + lp;  // the pixel's record index
           }
           n_pix += count(p != kIdle);
           chunk_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
@@ -302,7 +320,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           if (pix != kIdle) {
             pix_cost = 0;
             d = mk(r.x, r.y, r.z);
-            o = f.origin;
+            o = multi ? a.cams[chunk_frame].origin : f.origin;
             t = 0.f;
             it = 0;
             phase = kPrimary;
@@ -405,20 +423,24 @@ __global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
   const uint32_t lr = idx / width, x = idx - lr * width;
   const uint32_t y = band_row_to_global(a.g, lr);
   if (y >= a.f.height) return;
-  const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[idx]);
-  if (a.pixel_key) a.pixel_key[idx] = (uint8_t)(r1.y >> kRecKeyShift);  // coalesced, for the next frame's order
+  const uint32_t fr = blockIdx.y;  // frame of a multi-frame launch (0 otherwise)
+  const uint32_t rec = fr * a.rec_stride + idx;
+  const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[rec]);
+  // coalesced, for the next launch's order (a multi-frame launch: its last frame's costs)
+  if (a.pixel_key && fr + 1u == a.batch) a.pixel_key[idx] = (uint8_t)(r1.y >> kRecKeyShift);
   uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
   if (r1.y & kRecHit) {
-    const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[idx]);
-    const v3 dir = camera_ray(a.f, x, y);
-    const v3 hp = ray_at(a.f.origin, r0.x, dir);
+    const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[rec]);
+    const bool multi = a.batch > 1u;
+    const v3 dir = multi ? camera_ray_rows(a.f, a.cams[fr].row, x, y) : camera_ray(a.f, x, y);
+    const v3 hp = ray_at(multi ? a.cams[fr].origin : a.f.origin, r0.x, dir);
     const v3 n = mk(r0.y, r0.z, r0.w);
     float spec;
     v3 color = shade_hit_pre(a.f, scene_color<FAM>(hp), dir, n, r1.y & kRecStepsMask, &spec);
     color = shade_hit_post(color, spec, (r1.y & kRecSunMiss) ? -kInfinity : 0.0f, __uint_as_float(r1.x));
     word = pack_rgba(color, table);
   }
-  a.out[idx] = word;
+  a.out[(size_t)fr * a.out_stride + idx] = word;
 }
 
 // dst row y <- band b = y / band_rows, held by rank b % ranks as its (b / ranks)-th band.

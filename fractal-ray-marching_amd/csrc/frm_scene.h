@@ -392,16 +392,26 @@ FRM_HD v3 scene_color(v3 p) {
 FRM_HD float screen_x(uint32_t x, uint32_t w) { return (float)(2u * x + 1u) / (float)w - 1.0f; }
 FRM_HD float screen_y(uint32_t y, uint32_t h) { return 1.0f - (float)(2u * y + 1u) / (float)h; }
 
-// (vec4(d, 0) * camera_matrix).xyz, fragment.wgsl:315-325; dot4 = fma chain.
-FRM_HD v3 camera_ray(const FrameUniforms& f, uint32_t x, uint32_t y) {
+// (vec4(d, 0) * camera_matrix).xyz, fragment.wgsl:315-325; dot4 = fma chain. `row` = the
+// camera_matrix rows of the frame (f.row, or one frame's of a batch).
+FRM_HD v3 camera_ray_rows(const FrameUniforms& f, const float (&row)[3][4], uint32_t x, uint32_t y) {
   float sx = screen_x(x, f.width), sy = screen_y(y, f.height);
   v3 d = normalize(mk(sx * f.aspect_x, sy * f.aspect_y, kCameraDirectionZ));
   v3 o;
-  o.x = fma_(0.0f, f.row[0][3], fma_(d.z, f.row[0][2], fma_(d.y, f.row[0][1], d.x * f.row[0][0])));
-  o.y = fma_(0.0f, f.row[1][3], fma_(d.z, f.row[1][2], fma_(d.y, f.row[1][1], d.x * f.row[1][0])));
-  o.z = fma_(0.0f, f.row[2][3], fma_(d.z, f.row[2][2], fma_(d.y, f.row[2][1], d.x * f.row[2][0])));
+  o.x = fma_(0.0f, row[0][3], fma_(d.z, row[0][2], fma_(d.y, row[0][1], d.x * row[0][0])));
+  o.y = fma_(0.0f, row[1][3], fma_(d.z, row[1][2], fma_(d.y, row[1][1], d.x * row[1][0])));
+  o.z = fma_(0.0f, row[2][3], fma_(d.z, row[2][2], fma_(d.y, row[2][1], d.x * row[2][0])));
   return o;
 }
+FRM_HD v3 camera_ray(const FrameUniforms& f, uint32_t x, uint32_t y) { return camera_ray_rows(f, f.row, x, y); }
+
+// The camera of one frame of a multi-frame launch (frm_render_bands_batch): the rows of its
+// camera_matrix and transform_position(Position(0)). Frames of a batch share everything
+// else (size, aspect, step cap, scene uniforms).
+struct FrameCamera {
+  float row[3][4];
+  v3 origin;
+};
 
 // ---- shading helpers (fragment.wgsl:336-346) ----------------------------------------
 FRM_HD v3 to_sun() { return mk(kToSunX, kToSunY, kToSunZ); }

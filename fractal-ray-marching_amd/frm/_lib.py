@@ -23,6 +23,7 @@ FRM_ERR_COMPILE = 8
 
 FRM_NUM_SCENES = 19
 FRM_MAX_FRAMES_IN_FLIGHT = 8
+FRM_MAX_BATCH = 8
 FRM_DEFAULT_MAX_STEPS = 5000
 FRM_MAX_STEPS_LIMIT = 4194303
 FRM_MAX_NUM_ITERATIONS = 0xFFFFFFFF
@@ -120,6 +121,9 @@ SIGNATURES = [
     ("frm_render_bands", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("frm_render_bands_batch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("frm_unshuffle_bands", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),

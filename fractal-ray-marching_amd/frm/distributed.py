@@ -19,7 +19,7 @@ from . import tiling
 
 class RowTiledFrame:
     def __init__(self, width, height, rank, world, band_rows, device, render_bands, unshuffle,
-                 group=None, inflight=1, streams=None, collective=None, stage_host=None):
+                 group=None, inflight=1, streams=None, collective=None, stage_host=None, batch=1):
         """render_bands(buf, band_rows, first_band, band_stride, slot): enqueue the render of
         this rank's bands into the uint8 tensor buf (device memory for the GPU path) for
         frame slot `slot` (k % inflight; the GPU path renders it on streams[slot]).
@@ -29,6 +29,10 @@ class RowTiledFrame:
         the CPU tests), so up to `inflight` frames overlap on the GPU. collective: gather
         through torch.distributed (default: when world > 1; True with world 1 runs the
         same gather/unshuffle path on one rank, a test hook for RCCL on one GPU).
+        batch: frames per launch (frm_render_bands_batch): render_bands(buf, ...) renders the
+        next `batch` frames into buf, frame b at b * nbytes, one frame's bands each; one gather
+        moves them all; unshuffle(gathered, rank_stride, frame, slot) rebuilds one frame from
+        rank-major buffers rank_stride bytes apart.
         stage_host: gather through host copies of the band buffers (default: when the
         backend is gloo and the buffers live on a GPU). A test hook: RCCL refuses two ranks
         on one GPU, so a 1-GPU box runs the row split with gloo, whose gather takes host
@@ -48,19 +52,21 @@ class RowTiledFrame:
             stage_host = (self.collective and torch.device(device).type == "cuda"
                           and dist.get_backend(group) == "gloo")
         self.stage_host = bool(stage_host)
+        self.batch = max(1, batch)
         self.rows_local = tiling.rank_buffer_rows(height, band_rows, world)
-        self.nbytes = self.rows_local * width * 4
+        self.nbytes = self.rows_local * width * 4  # one frame's bands (padded)
         # buffer k % nbuf serves frame k. Reuse is safe in stream order: frame k + nbuf runs
         # on frame k's stream (nbuf is a multiple of inflight), after frame k's gather wait
         # and unshuffle, which _finish(k) enqueues before frame k + nbuf is issued.
         nbuf = self.inflight if self.inflight > 1 else (2 if self.collective else 1)
         self.nbuf = nbuf
-        self.bufs = [torch.zeros(self.nbytes, dtype=torch.uint8, device=device) for _ in range(nbuf)]
+        B = self.batch
+        self.bufs = [torch.zeros(B * self.nbytes, dtype=torch.uint8, device=device) for _ in range(nbuf)]
         self.gathered = self.frames = None
         if self.collective and rank == 0:
-            self.gathered = [torch.zeros(world * self.nbytes, dtype=torch.uint8, device=device)
+            self.gathered = [torch.zeros(world * B * self.nbytes, dtype=torch.uint8, device=device)
                              for _ in range(nbuf)]
-            self.frames = [torch.zeros(height * width * 4, dtype=torch.uint8, device=device)
+            self.frames = [torch.zeros(B * height * width * 4, dtype=torch.uint8, device=device)
                            for _ in range(nbuf)]
         self.frames_done = 0
         self.last = 0
@@ -87,7 +93,8 @@ class RowTiledFrame:
                     g.copy_(torch.cat(glist))
                 return None
             if self.rank == 0:
-                glist = [g[i * self.nbytes:(i + 1) * self.nbytes] for i in range(self.world)]
+                n = self.batch * self.nbytes
+                glist = [g[i * n:(i + 1) * n] for i in range(self.world)]
             return dist.gather(buf, gather_list=glist, dst=0, group=self.group, async_op=True)
 
     def _finish(self, k, work):
@@ -96,19 +103,26 @@ class RowTiledFrame:
                 if work is not None:
                     work.wait()  # NCCL: the stream waits for the gather (the host does not)
                 if self.rank == 0:
-                    self.unshuffle(self.gathered[k % self.nbuf], self.frames[k % self.nbuf],
-                                   k % self.inflight)
+                    g, fr = self.gathered[k % self.nbuf], self.frames[k % self.nbuf]
+                    fb = self.height * self.width * 4
+                    for b in range(self.batch):  # frame b of the batch: rank r's at r*B*nbytes + b*nbytes
+                        self.unshuffle(g[b * self.nbytes:], self.batch * self.nbytes, fr[b * fb:(b + 1) * fb],
+                                       k % self.inflight)
         self.last = k % self.nbuf
-        self.frames_done += 1
+        self.frames_done += self.batch
 
     def run(self, n, before_frame=None):
         """Render, gather and reassemble n frames (asynchronous on the GPU path: callers
-        synchronize the device to wait for the last one). before_frame(k), if given, runs on
-        the host before frame k is issued (e.g. to advance animated parameters)."""
+        synchronize the device to wait for the last one; n a multiple of batch).
+        before_frame(k), if given, runs on the host before frame k is issued (e.g. to advance
+        animated parameters); for a batch, before each of its frames, before the launch."""
+        if n % self.batch:
+            raise ValueError(f"{n} frames is not a multiple of the batch ({self.batch})")
         pending = None
-        for k in range(n):
+        for k in range(n // self.batch):
             if before_frame is not None:
-                before_frame(k)
+                for j in range(self.batch):
+                    before_frame(k * self.batch + j)
             work = self._issue(k)
             if pending is not None:
                 self._finish(*pending)
@@ -119,5 +133,6 @@ class RowTiledFrame:
     def output(self):
         """Rank 0: the last frame, flat RGBA8 (the band buffer itself when world == 1)."""
         if not self.collective:
-            return self.bufs[self.last]
-        return self.frames[self.last]
+            return self.bufs[self.last][(self.batch - 1) * self.nbytes:]
+        fb = self.height * self.width * 4
+        return self.frames[self.last][(self.batch - 1) * fb:]

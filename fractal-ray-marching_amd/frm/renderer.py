@@ -103,6 +103,18 @@ class Renderer:
         self._check(self._lib.frm_render_bands(self.ctx, dev_ptr, nbytes, band_rows, first_band,
                                                band_stride, stream or None, dev_counters or None))
 
+    def render_bands_batch(self, params_list, dev_ptr, frame_stride, band_rows, first_band, band_stride,
+                           stream=0, dev_counters=0):
+        """frm_render_bands_batch: len(params_list) frames (same scene, camera may differ) in
+        one launch, frame k at dev_ptr + k * frame_stride."""
+        from ._lib import FrmParameters
+        arr = (FrmParameters * len(params_list))()
+        for k, p in enumerate(params_list):
+            ctypes.memmove(ctypes.addressof(arr[k]), p.to_bytes(), ctypes.sizeof(FrmParameters))
+        self._check(self._lib.frm_render_bands_batch(self.ctx, len(params_list), ctypes.addressof(arr), dev_ptr,
+                                                     frame_stride, band_rows, first_band, band_stride,
+                                                     stream or None, dev_counters or None))
+
     def unshuffle_bands(self, src_ptr, rank_stride, dst_ptr, dst_bytes, band_rows, ranks, stream=0):
         self._check(self._lib.frm_unshuffle_bands(self.ctx, src_ptr, rank_stride, dst_ptr, dst_bytes,
                                                   band_rows, ranks, stream or None))

@@ -208,6 +208,21 @@ int frm_band_rows_for(uint32_t height, uint32_t band_rows, uint32_t first_band,
 int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t band_rows,
                      uint32_t first_band, uint32_t band_stride, void* stream,
                      uint64_t* dev_counters);
+/* Multi-frame launch: renders `count` frames (1..FRM_MAX_BATCH) of the context's size in ONE
+ * launch, frame k with params[k], each as frm_render_bands would render it (this rank's bands,
+ * band-major) into dev_dst + k * frame_stride_bytes. The frames' pixels share one work queue
+ * (each frame's pixels longest first, the frames interleaved), so one frame's longest pixels
+ * run beside the other frames' work instead of ending a launch with idle lanes: for short
+ * launches (a rank's share of a row-split frame) the persistent kernel's tail is paid once
+ * per batch. The frames may differ in camera only: params[k] must give the same scene,
+ * num_iterations, time-derived scene constants and aspect as params[0]
+ * (FRM_ERR_INVALID_ARGUMENT otherwise). The context's parameters become params[count-1].
+ * Counters are added over all frames. Bytes per frame are those of frm_render_bands. */
+#define FRM_MAX_BATCH 8u
+int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* params,
+                           uint8_t* dev_dst, size_t frame_stride_bytes, uint32_t band_rows,
+                           uint32_t first_band, uint32_t band_stride, void* stream,
+                           uint64_t* dev_counters);
 /* Reassemble a frame from per-rank band buffers laid out rank-major in dev_src
  * (rank r's buffer starts at r*rank_stride_bytes, as written by frm_render_bands with
  * first_band = r, band_stride = ranks) into row-major dev_dst. Asynchronous. */

@@ -27,7 +27,7 @@ def _times():
     return [frm.POWER8_TIME + 0.75 * k for k in range(3)]  # a different frame each time
 
 
-def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None):
+def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None, batch=1):
     for p in (ROOT, os.path.join(ROOT, "fractal-ray-marching_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     import frm
@@ -40,26 +40,31 @@ def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None):
     state = {"p": None}
     counters = np.zeros(8, np.int64)
 
+    state["ps"] = []
+
     def before_frame(k):
-        state["p"] = params_for(18, 8, _times()[k], W, H)
+        state["ps"].append(params_for(18, 8, _times()[k], W, H))
 
     def render_bands(buf, br, first, stride, slot):
         assert 0 <= slot < inflight
-        p = state["p"]
         rows = tiling.global_rows(H, br, first, stride)
         valid = [y for y in rows if y >= 0]
-        r = frm_oracle.render(p, W, H, 128, rows=valid, threads=2)
-        out = buf.numpy().reshape(-1, W, 4)
-        out[:len(valid)] = r["rgba"]  # padding rows (y < 0) are only at the end
-        counters[:] += r["counters"].astype(np.int64)
+        nb = len(rows) and tiling.rank_buffer_rows(H, br, stride) * W * 4
+        for b, p in enumerate(state["ps"][-batch:]):  # the batch's frames, in order
+            r = frm_oracle.render(p, W, H, 128, rows=valid, threads=2)
+            out = buf.numpy()[b * nb:(b + 1) * nb].reshape(-1, W, 4)
+            out[:len(valid)] = r["rgba"]  # padding rows (y < 0) are only at the end
+            counters[:] += r["counters"].astype(np.int64)
 
-    def unshuffle(gathered, frame, slot):
-        g = gathered.numpy().reshape(world, -1, W, 4)
+    def unshuffle(gathered, rank_stride, frame, slot):
+        nb = tiling.rank_buffer_rows(H, br_used, world) * W * 4
+        raw = gathered.numpy()
+        g = np.stack([raw[r * rank_stride:r * rank_stride + nb] for r in range(world)]).reshape(world, -1, W, 4)
         frame.numpy()[:] = tiling.unshuffle(g, H, br_used, world).reshape(-1)
 
     br_used = band_rows
     tf = RowTiledFrame(W, H, rank, world, band_rows, "cpu", render_bands, unshuffle, inflight=inflight,
-                        stage_host=stage_host)
+                        stage_host=stage_host, batch=batch)
     assert tf.stage_host == bool(stage_host)
     tf.run(3, before_frame)
     c = torch.from_numpy(counters.copy())
@@ -70,18 +75,19 @@ def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W,H,band_rows,inflight,stage_host", [(48, 27, 4, 1, None), (40, 24, 6, 1, None),
-                                                               (48, 27, 4, 2, None), (40, 24, 6, 3, None),
-                                                               (40, 24, 6, 3, True)])
-def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows, inflight, stage_host):
-    """stage_host=True: the host-staged gather bench.py uses for gloo ranks on one GPU."""
+@pytest.mark.parametrize("W,H,band_rows,inflight,stage_host,batch", [
+    (48, 27, 4, 1, None, 1), (40, 24, 6, 1, None, 1), (48, 27, 4, 2, None, 1), (40, 24, 6, 3, None, 1),
+    (40, 24, 6, 3, True, 1), (48, 27, 4, 1, None, 3), (40, 24, 6, 2, True, 3)])
+def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows, inflight, stage_host, batch):
+    """stage_host=True: the host-staged gather bench.py uses for gloo ranks on one GPU;
+    batch=3: the three frames rendered by one multi-frame launch per rank, one gather."""
     from helpers import params_for
     import frm
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, inflight, q, stage_host)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, band_rows, inflight, q, stage_host, batch)) for r in range(2)]
     for pr in procs:
         pr.start()
     frame, counters, frames = q.get(timeout=180)

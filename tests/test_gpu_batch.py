@@ -1,0 +1,90 @@
+"""Multi-frame launches (frm_render_bands_batch): several frames of one scene whose cameras
+differ render in one persistent launch (one work queue, frames interleaved chunk by chunk),
+each frame byte-identical to the oracle's render of its own Parameters; counters are the
+frames' sums. Whole frames and a simulated 2-rank band split, several consecutive batches
+(the scheduled order of the previous batch's last frame), 1 and 2 frames in flight."""
+import numpy as np
+import pytest
+
+import frm
+from frm import _lib, tiling
+from helpers import params_for
+
+pytestmark = pytest.mark.gpu
+
+
+def _poses(scene, iters, time, w, h):
+    return [params_for(scene, iters, time, w, h, pose=pz) for pz in ("P0", "P1", "P2", "P1")]
+
+
+@pytest.mark.parametrize("scene,iters,steps", [(18, 12, 256), (0, 5, 128), (16, 4, 128)])
+@pytest.mark.parametrize("inflight", [1, 2])
+def test_batch_whole_frames_bit_exact(frm_lib, oracle, scene, iters, steps, inflight):
+    import torch
+
+    w, h = 96, 54
+    ps = _poses(scene, iters, frm.POWER8_TIME, w, h)
+    refs = [oracle.render(p, w, h, steps) for p in ps]
+    fb = w * h * 4
+    dev = torch.device("cuda", 0)
+    out = torch.zeros(len(ps) * fb, dtype=torch.uint8, device=dev)
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    with frm.Renderer(device=0, max_steps=steps, flags=frm.FRM_FLAG_PERSISTENT_KERNEL, frames_in_flight=inflight) as r:
+        r.resize(w, h)
+        for rep in range(3):  # the second and third batches fetch in the scheduled order
+            counters.zero_()
+            out.zero_()
+            r.render_bands_batch(ps, out.data_ptr(), fb, h, 0, 1, 0, counters.data_ptr())
+            torch.cuda.synchronize()
+            img = out.cpu().numpy().reshape(len(ps), h, w, 4)
+            for k, ref in enumerate(refs):
+                assert np.array_equal(img[k], ref["rgba"]), f"batch {rep} frame {k}"
+            got = [int(v) for v in counters.cpu().tolist()][:7]
+            assert got == [sum(int(ref["counters"][i]) for ref in refs) for i in range(7)]
+
+
+def test_batch_band_split_bit_exact(frm_lib, oracle):
+    """Two simulated ranks, each rendering its interleaved bands of 3 frames in one launch;
+    frame b reassembled from the rank-major buffers (rank stride = batch x bands)."""
+    import torch
+
+    w, h, ranks, br = 80, 45, 2, 8
+    ps = _poses(18, 12, frm.POWER8_TIME, w, h)[:3]
+    B = len(ps)
+    nb = tiling.rank_buffer_rows(h, br, ranks) * w * 4
+    dev = torch.device("cuda", 0)
+    gathered = torch.zeros(ranks * B * nb, dtype=torch.uint8, device=dev)
+    rds = [frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL) for _ in range(ranks)]
+    try:
+        for rep in range(2):
+            for rk, rd in enumerate(rds):
+                rd.resize(w, h)
+                rd.render_bands_batch(ps, gathered.data_ptr() + rk * B * nb, nb, br, rk, ranks)
+            torch.cuda.synchronize()
+            for b, p in enumerate(ps):
+                frame = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
+                rds[0].unshuffle_bands(gathered.data_ptr() + b * nb, B * nb, frame.data_ptr(), frame.numel(), br, ranks)
+                torch.cuda.synchronize()
+                ref = oracle.render(p, w, h, 256)
+                assert np.array_equal(frame.cpu().numpy().reshape(h, w, 4), ref["rgba"]), f"rep {rep} frame {b}"
+    finally:
+        for rd in rds:
+            rd.close()
+
+
+def test_batch_rejects_frames_that_differ_beyond_the_camera(frm_lib):
+    import torch
+
+    w, h = 32, 18
+    a = params_for(18, 12, frm.POWER8_TIME, w, h)
+    b = params_for(18, 12, frm.POWER8_TIME + 1.0, w, h)  # another time: another power
+    c = params_for(18, 11, frm.POWER8_TIME, w, h)        # other iteration count
+    buf = torch.zeros(2 * w * h * 4, dtype=torch.uint8, device="cuda")
+    with frm.Renderer(device=0, max_steps=64) as r:
+        r.resize(w, h)
+        for other in (b, c):
+            with pytest.raises(frm.FrmError) as e:
+                r.render_bands_batch([a, other], buf.data_ptr(), w * h * 4, h, 0, 1)
+            assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
+        with pytest.raises(frm.FrmError):
+            r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), w * h * 4, h, 0, 1)

@@ -114,8 +114,8 @@ def test_rccl_gather_pipeline_one_rank(frm_lib, refs):
                 r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, streams[slot].cuda_stream,
                                counters.data_ptr())
 
-            def unshuffle(gathered, frame, slot):
-                r.unshuffle_bands(gathered.data_ptr(), gathered.numel(), frame.data_ptr(), frame.numel(),
+            def unshuffle(gathered, rank_stride, frame, slot):
+                r.unshuffle_bands(gathered.data_ptr(), rank_stride, frame.data_ptr(), frame.numel(),
                                   band_rows, 1, streams[slot].cuda_stream)
 
             tf = RowTiledFrame(W, H, 0, 1, band_rows, dev, render_bands, unshuffle, inflight=F, streams=streams,

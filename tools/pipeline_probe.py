@@ -31,7 +31,8 @@ def cumask_stream(dev):
     return torch.cuda.ExternalStream(st.value, device=dev)
 
 
-def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=False, cumask=False, gather=False):
+def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=False, cumask=False, gather=False,
+        batch=1):
     """mode 'slots': one context with frames_in_flight = F; 'contexts': F contexts."""
     w = frm.WORKLOADS[workload]
     p = frm.make_parameters(w, pose="P1")
@@ -54,7 +55,7 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
             r = one
         rs.append(r)
         ss.append(cumask_stream(dev) if cumask else torch.cuda.Stream(device=dev))
-        bufs.append(torch.zeros(rows * w.width * 4, dtype=torch.uint8, device=dev))
+        bufs.append(torch.zeros(batch * rows * w.width * 4, dtype=torch.uint8, device=dev))
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     # gather: rank 0's extra work per frame of a real P-way run, on its render stream after its
     # bands: P - 1 rank buffers arriving (device-to-device copies of its own buffer stand in
@@ -62,23 +63,31 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
     gbufs = frames_out = None
     if gather and ranks > 1:
         gbufs = [torch.zeros(ranks * bufs[0].numel(), dtype=torch.uint8, device=dev) for _ in range(inflight)]
-        frames_out = [torch.zeros(w.width * w.height * 4, dtype=torch.uint8, device=dev) for _ in range(inflight)]
+        frames_out = [torch.zeros(batch * w.width * w.height * 4, dtype=torch.uint8, device=dev)
+                      for _ in range(inflight)]
+    fbytes = rows * w.width * 4
 
     def go(n):
         for k in range(n):
             i = k % inflight
             if events:
                 torch.cuda.Event(enable_timing=True).record(ss[i])
-            rs[i].render_bands(bufs[i].data_ptr(), bufs[i].numel(), br, rank, ranks, ss[i].cuda_stream,
-                               counters.data_ptr())
+            if batch > 1:
+                rs[i].render_bands_batch([p] * batch, bufs[i].data_ptr(), fbytes, br, rank, ranks, ss[i].cuda_stream,
+                                         counters.data_ptr())
+            else:
+                rs[i].render_bands(bufs[i].data_ptr(), bufs[i].numel(), br, rank, ranks, ss[i].cuda_stream,
+                                   counters.data_ptr())
             if gbufs is not None:
                 with torch.cuda.stream(ss[i]):
                     nb = bufs[i].numel()
                     gbufs[i][:nb].copy_(bufs[i])
                     for q in range(1, ranks):
                         gbufs[i][q * nb:(q + 1) * nb].copy_(bufs[i], non_blocking=True)
-                rs[i].unshuffle_bands(gbufs[i].data_ptr(), nb, frames_out[i].data_ptr(), frames_out[i].numel(),
-                                      br, ranks, ss[i].cuda_stream)
+                fb = w.width * w.height * 4
+                for b in range(batch):
+                    rs[i].unshuffle_bands(gbufs[i].data_ptr() + b * fbytes, nb, frames_out[i].data_ptr() + b * fb, fb,
+                                          br, ranks, ss[i].cuda_stream)
             if events:
                 torch.cuda.Event(enable_timing=True).record(ss[i])
 
@@ -86,14 +95,15 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
     torch.cuda.synchronize()
     counters.zero_()
     t0 = time.perf_counter()
-    go(frames)
+    go(frames // batch)  # launches
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    frames = frames // batch * batch
     st = rs[0].stats_from_counters([int(v) for v in counters.cpu().tolist()])
     for r in set(rs):
         r.close()
     return {"workload": workload, "ranks": ranks, "rank": rank, "inflight": inflight, "mode": mode, "events": events, "cumask": cumask,
-            "gather": bool(gbufs is not None),
+            "gather": bool(gbufs is not None), "batch": batch,
             "ms_per_frame": dt / frames * 1e3, "gsteps": st["march_steps"] / dt / 1e9}
 
 
@@ -109,6 +119,7 @@ def main():
     ap.add_argument("--repeat", type=int, default=1)
     ap.add_argument("--rank-ids", default="0", help="ranks whose share to time ('all' = every rank)")
     ap.add_argument("--gather", default="0", help="1: rank 0 also receives and unshuffles (see run())")
+    ap.add_argument("--batch", default="1", help="frames per launch (frm_render_bands_batch)")
     args = ap.parse_args()
     for wl in args.workloads.split(","):
         for P in [int(x) for x in args.ranks.split(",")]:
@@ -121,8 +132,10 @@ def main():
                                 for g in [bool(int(x)) for x in args.gather.split(",")]:
                                     if g and rk != 0:
                                         continue
-                                    for _ in range(args.repeat):
-                                        print(json.dumps(run(wl, P, rk, F, args.frames, 2, m, ev, cm, g)), flush=True)
+                                    for B in [int(x) for x in args.batch.split(",")]:
+                                        for _ in range(args.repeat):
+                                            print(json.dumps(run(wl, P, rk, F, args.frames, 2, m, ev, cm, g, B)),
+                                                  flush=True)
 
 
 if __name__ == "__main__":
