@@ -159,8 +159,10 @@ def pmc_summary(workload, world):
         if s.get("source_sha256") != cur:
             stale = stale or os.path.relpath(path, ROOT)
             continue
+        B = s.get("frames_per_dispatch", 1)
         return {
-            "traffic": s["hbm_read_bytes"] + s["hbm_write_bytes"],
+            # HBM bytes per frame of the dominant kernel (a dispatch renders B frames)
+            "traffic": (s["hbm_read_bytes"] + s["hbm_write_bytes"]) / B,
             "valu_busy": s["valu_busy"],
             "valu_lane_utilization": s["valu_lane_utilization"],
             "hbm_write_gbps": s["hbm_write_gbps"],

@@ -38,6 +38,17 @@ def load(d, name):
     return dict(out)
 
 
+def frames_per_dispatch(d):
+    """bench.py's frames per launch in the profiled run (its JSON line, written by pmc.sh)."""
+    for n in ("sq", "wr", "rd", "sq2"):
+        try:
+            with open(f"{d}/{n}.json") as fh:
+                return int(json.loads(fh.read().strip().splitlines()[-1])["config"].get("frames_per_launch", 1))
+        except (OSError, ValueError, KeyError, IndexError):
+            continue
+    return 1
+
+
 def main(d):
     c = {}
     for n in ("sq", "sq2", "wr", "rd"):
@@ -51,7 +62,9 @@ def main(d):
     dur = dur[SKIP:] or dur
     t = sum(dur) / len(dur)
     grbm_xcd = c["GRBM_GUI_ACTIVE"] / 8
+    B = frames_per_dispatch(d)
     s = {
+        "frames_per_dispatch": B,
         "kernel_s_profiled": t,
         "clock_ghz": grbm_xcd / t / 1e9,
         "valu_wave_insts": c["SQ_INSTS_VALU"],
@@ -63,6 +76,10 @@ def main(d):
         "hbm_write_bytes": c.get("WRITE_SIZE", 0) * 1024,
         "hbm_read_bytes": 2 * c.get("FETCH_SIZE", 0) * 1024,
         "hbm_write_gbps": c.get("WRITE_SIZE", 0) * 1024 / t / 1e9,
+        # per frame of the dispatch (a multi-frame launch renders B frames per dispatch)
+        "hbm_write_bytes_per_frame": c.get("WRITE_SIZE", 0) * 1024 / B,
+        "hbm_read_bytes_per_frame": 2 * c.get("FETCH_SIZE", 0) * 1024 / B,
+        "kernel_s_per_frame_profiled": t / B,
         "dispatches_averaged": len(dur),
         # the kernel sources these counters were measured on (bench.py cites only a match)
         "source_sha256": provenance.source_sha256(),

@@ -1,6 +1,7 @@
-"""Per-frame device time of the LAST k frames of a rocprofv3 kernel trace (the bench's timed
+"""Per-frame device time of the LAST k launches of a rocprofv3 kernel trace (the bench's timed
 region: `bench.py --steps k` runs warmup frames first), to compare with bench.py's live
-HIP-event roofline.avg_kernel_ms.
+HIP-event roofline.avg_kernel_ms. With B frames per launch (bench --batch; argv[3]) the
+times are divided by B: per frame.
 
 With frames in flight (bench.py --inflight F > 1) the frames' kernels overlap, so the
 per-frame time is the SPAN of the last k frames' dispatches (first start to last end) / k,
@@ -17,7 +18,7 @@ def kind(n):
             else "radix_sort" if "radix_sort" in n else None)
 
 
-def main(trace, k):
+def main(trace, k, batch=1):
     rows = []
     for r in csv.DictReader(open(trace)):
         name = kind(r["Kernel_Name"])
@@ -33,9 +34,10 @@ def main(trace, k):
         d = per.get(name, [])
         per_frame = len(d) // max(calls, 1) if calls else 1  # radix sort: several dispatches per frame
         last = d[-k * max(per_frame, 1):]
-        avg = sum(last) / k if last else 0.0
+        avg = sum(last) / k / batch if last else 0.0
         total += avg
-        print(f"{name:18s} last {k} frames: {avg:.3f} ms per frame ({len(d)} dispatches in the trace)")
+        print(f"{name:18s} last {k} launches: {avg:.3f} ms per frame ({len(d)} dispatches in the trace, "
+              f"{batch} frames per launch)")
     print(f"{'sum':18s} {total:.3f} ms per frame (sum of dispatch durations)")
     # span: from the first dispatch of the first timed frame's march (minus its sort) to the
     # end of the last dispatch
@@ -46,8 +48,9 @@ def main(trace, k):
         t0 = sorts_before[-1] if sorts_before else first
         t0 = min([t0] + [s for s, e, n in rows if s >= t0])
         t1 = max(e for s, e, n in rows if s >= t0)
-        print(f"{'span':18s} {(t1 - t0) / 1e6 / k:.3f} ms per frame (first start to last end of the last {k} frames)")
+        print(f"{'span':18s} {(t1 - t0) / 1e6 / k / batch:.3f} ms per frame (first start to last end of the last "
+              f"{k} launches)")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 5)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 5, int(sys.argv[3]) if len(sys.argv) > 3 else 1)
