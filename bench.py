@@ -270,15 +270,15 @@ def main():
     # pixels a launch has (measured: 4K/8K whole frames best at 2, 1080p and a rank's share
     # of a split frame at 3)
     # frames per launch: the frames' pixels share one work queue, so a launch's tail (its
-    # costliest pixels' sequential marches) is paid once per batch (measured, DESIGN.md section 7:
-    # 8-way rank share 1.67 ms/frame at 1 frame per launch and 3 in flight -> 1.38-1.44 at 8 per
-    # launch and 2 in flight; whole 4K frame 11.20 -> 10.89 ms at 4 per launch; 1080p 3.12 ->
-    # 2.81). Animated workloads change the scene every frame and render one frame per launch.
-    batch = 1 if w.animated else max(1, min(args.batch or (8 if split > 1 else 4), frm.FRM_MAX_BATCH))
+    # costliest pixels' sequential marches) is paid once per batch (measured, DESIGN.md sections
+    # 6-7: 8-way rank share 1.67 ms/frame at 1 frame per launch and 3 in flight -> 1.38-1.44 at
+    # 8 per launch and 2 in flight; whole 4K frame 11.20 -> 10.84 ms at 8 per launch, 1080p
+    # 3.12 -> 2.80). Animated workloads change the scene every frame: one frame per launch.
+    batch = 1 if w.animated else max(1, min(args.batch or 8, frm.FRM_MAX_BATCH))
     if args.inflight:
         inflight = args.inflight
     elif batch > 1:
-        inflight = 2 if split > 1 or local_pixels < 4_000_000 else 1
+        inflight = 2 if split > 1 else 1
     else:
         inflight = 3 if split > 1 or local_pixels < 4_000_000 else 2
     inflight = max(1, min(inflight, frm.FRM_MAX_FRAMES_IN_FLIGHT))
