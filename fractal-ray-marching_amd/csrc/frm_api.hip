@@ -610,14 +610,35 @@ extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
   const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
   return hipMemcpy(out5, sl.queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
+#endif
+
 // per-pixel cost keys recorded by the last persistent launch (local pixel order; before
 // the next launch overwrites them)
-extern "C" int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
+int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
+  if (!ctx || !out) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
   const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
+  if (!sl.sched_keys) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "no persistent launch yet");
   if (n > sl.sched_cap) n = sl.sched_cap;
-  return hipMemcpy(out, sl.sched_keys, n, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  FRM_HIP(ctx, hipDeviceSynchronize());
+  FRM_HIP(ctx, hipMemcpy(out, sl.sched_keys, n, hipMemcpyDeviceToHost));
+  return (int)n;
 }
-#endif
+
+// replaces the cost keys the next launch sorts its pixels by (scheduling experiments): the
+// slot of the next launch must hold the history of a whole frame of the current size
+int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
+  if (!ctx || !keys) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
+  Slot& sl = ctx->slots[ctx->next_slot];
+  if (!sl.sched_history || !sl.sched_whole || sl.sched_w != ctx->width || sl.sched_h != ctx->height ||
+      n != (size_t)ctx->width * ctx->height || n > sl.sched_cap)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "no whole-frame history of this size in the next slot");
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  int rc = wait_slot(ctx, sl);
+  if (rc) return rc;
+  FRM_HIP(ctx, hipMemcpy(sl.sched_keys, keys, n, hipMemcpyHostToDevice));
+  return FRM_OK;
+}
 
 int frm_stats_from_counters(const frm_ctx* ctx, const uint64_t* c, frm_stats* out) {
   if (!ctx || !c || !out) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "NULL argument");

@@ -132,6 +132,8 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("frm_eval_math", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("frm_debug_pixel_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("frm_debug_set_pixel_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_parameters_default", None, [_P(FrmParameters)]),
     ("frm_parameters_update_aspect", None, [_P(FrmParameters), ctypes.c_uint32, ctypes.c_uint32]),
     ("frm_parameters_update_time", None, [_P(FrmParameters), ctypes.c_float]),

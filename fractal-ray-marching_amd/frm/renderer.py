@@ -144,6 +144,21 @@ class Renderer:
                                             out.ctypes.data))
         return out
 
+    def pixel_keys(self):
+        """The 8-bit cost keys (16 log2(bodies + 1)) the last persistent launch recorded per
+        local pixel, row-major (scheduling diagnostics)."""
+        n = self.width * self.height
+        out = np.zeros(n, np.uint8)
+        got = self._lib.frm_debug_pixel_keys(self.ctx, out.ctypes.data, n)
+        if got < 0:
+            self._check(got)
+        return out[:got]
+
+    def set_pixel_keys(self, keys):
+        """Replace the cost keys the next persistent launch sorts its pixels by."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8)
+        self._check(self._lib.frm_debug_set_pixel_keys(self.ctx, k.ctypes.data, k.size))
+
     def stats_from_counters(self, counters):
         arr = (ctypes.c_uint64 * _lib.FRM_NUM_COUNTERS)(*[int(c) for c in counters])
         st = _lib.FrmStats()

@@ -252,6 +252,13 @@ int frm_eval_scene(frm_ctx* ctx, const float* points, uint32_t n, float* out_dis
                    float* out_color);
 int frm_eval_math(frm_ctx* ctx, int32_t fn, const float* a, const float* b, uint32_t n,
                   float* out);
+/* frm_debug_pixel_keys: the 8-bit scheduling cost keys (16 log2(bodies + 1), csrc/frm_sched.hip)
+ * the context's last persistent launch recorded per local pixel, row-major; copies
+ * min(n, pixels) bytes and returns that count, or a negative frm_status. */
+int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n);
+/* frm_debug_set_pixel_keys: replaces the keys the next persistent launch orders its pixels by
+ * (n = width x height; the next slot must hold a whole frame of the current size). */
+int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n);
 
 /* ---- host-side mirrors of the reference's Parameters mutators (src/parameters.rs).
  *      These let a C/C++/Python host drive the same uniform without Rust. */
