@@ -8,7 +8,6 @@
 #include <hip/hip_runtime.h>
 
 #include "frm_render_kernels.h"
-#include "frm_pool_kernel.h"
 
 namespace frm {
 
@@ -112,24 +111,6 @@ static int blocks_override() {  // experiments: FRM_BLOCKS_PER_CU
   return v >= 1 && v <= 64 ? v : 0;
 }
 
-// experiments: FRM_POOL=1 runs march_pool for the Mandelbulb (frm_pool_kernel.h), FRM_POOL_SWAP
-// its swap threshold (lanes that can swap before the body loop stops; default 8)
-static bool pool_kernel() {
-  static const int v = [] {
-    const char* env = getenv("FRM_POOL");
-    return env ? atoi(env) : 0;
-  }();
-  return v != 0;
-}
-static uint32_t pool_swap_min() {
-  static const uint32_t v = [] {
-    const char* env = getenv("FRM_POOL_SWAP");
-    const int x = env ? atoi(env) : 8;
-    return (uint32_t)(x >= 1 && x <= 64 ? x : 8);
-  }();
-  return v;
-}
-
 // A reloaded module's kernel (frm_reload.hip) takes the same KernelArgs by value.
 static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStream_t stream, const KernelArgs& args) {
   void* params[] = {const_cast<KernelArgs*>(&args)};
@@ -159,30 +140,6 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
     hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(kMarchBlock), stream, args);
     if (e != hipSuccess) return e;
     return module_launch(rk->shade[FAM], dim3((pixels + 255u) / 256u, args.batch), dim3(256), stream, args);
-  }
-  if constexpr (FAM == kMandelbulb && ITERS) {
-    if (pool_kernel()) {  // march_pool (frm_pool_kernel.h)
-      static int pool_bpc = 0;
-      if (pool_bpc == 0) {
-        int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_pool<false>, kMarchBlock, 0);
-        if (e != hipSuccess) return e;
-        pool_bpc = n > 0 ? n : 1;
-      }
-      // every wave fills 128 pool slots from its first two chunks
-      uint32_t pblocks = (uint32_t)((blocks_override() ? blocks_override() : pool_bpc) * cu_count);
-      const uint32_t pmax = ((positions + 2u * kChunk - 1u) / (2u * kChunk) + kMarchWaves - 1u) / kMarchWaves;
-      if (pblocks > pmax) pblocks = pmax;
-      if (pblocks == 0) pblocks = 1;
-      KernelArgs pa = args;
-      pa.service_min = pool_swap_min();
-      if (args.batch > 1)
-        hipLaunchKernelGGL((march_pool<true>), dim3(pblocks), dim3(kMarchBlock), 0, stream, pa);
-      else
-        hipLaunchKernelGGL((march_pool<false>), dim3(pblocks), dim3(kMarchBlock), 0, stream, pa);
-      hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u, args.batch), dim3(256), 0, stream, args);
-      return hipGetLastError();
-    }
   }
   if (args.batch > 1)
     hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
@@ -304,15 +261,5 @@ hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst
 extern "C" int frm_debug_waves(uint64_t* out, size_t slots) {
   if (slots > frm::kWaveDebugSlots) slots = frm::kWaveDebugSlots;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(frm::g_wave_debug), slots * 128) == hipSuccess ? (int)slots : -1;
-}
-#endif
-
-#ifdef FRM_POOL_STAMPS
-// diagnostic build: {wave cycles, service, swap, body-loop cycles, services, full services, swaps,
-// body iterations} summed over the waves of every march_pool launch since the last read
-extern "C" int frm_debug_pool(uint64_t* out8) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(frm::g_pool_debug), 64) != hipSuccess) return -1;
-  const unsigned long long zero[8] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(frm::g_pool_debug), zero, 64) == hipSuccess ? 0 : -1;
 }
 #endif
