@@ -675,7 +675,7 @@ int frm_eval_scene(frm_ctx* ctx, const float* points, uint32_t n, float* out_dis
 }
 
 int frm_eval_math(frm_ctx* ctx, int32_t fn, const float* a, const float* b, uint32_t n, float* out) {
-  if (!ctx || !a || !out || fn < 0 || fn > FRM_MATH_LOG_POSNORMAL) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad argument");
+  if (!ctx || !a || !out || fn < 0 || fn > FRM_MATH_SRGB_ENCODE) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad argument");
   if (n == 0) return FRM_OK;
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   float* d = nullptr;

@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void eval_math(int fn, const float* a, const f
     case 16: r = atan2_tame(x, y); break;
     case 17: r = log2_tame(x); break;
     case 18: r = exp2_tame(x); break;
-    default: r = log_posnormal(x); break;
+    case 19: r = log_posnormal(x); break;
+    default: r = (float)encode_srgb(x, kSrgbThresholds); break;
 #else
     default: r = x; break;
 #endif
@@ -180,7 +181,7 @@ hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, 
 // magnification and nearest minification (persistent_graphics.rs:55-64). The texture is
 // Rgba8UnormSrgb, so texels are decoded to linear light before filtering; the surface's
 // format decides the output encoding (FRM_BLIT_SRGB) and byte order (FRM_BLIT_BGRA).
-// One thread per output pixel, 16x16 pixels per block.
+// One thread per output column of four pixels (rows 16 apart), 16 x 64 output pixels per block.
 __device__ __forceinline__ float blit_mix(float a, float b, float t) { return a * (1.0f - t) + b * t; }
 
 __device__ __forceinline__ uint32_t blit_channel(float c, bool srgb, const float* table) {
@@ -188,53 +189,60 @@ __device__ __forceinline__ uint32_t blit_channel(float c, bool srgb, const float
   return (uint32_t)rintf(fminf(fmaxf(c, 0.0f), 1.0f) * 255.0f);      // unorm, NaN -> 0
 }
 
+constexpr uint32_t kBlitRows = 4;  // output rows per thread (16 x 64 output pixels per block)
+
 __global__ __launch_bounds__(256) void blit_kernel(const uint32_t* __restrict__ src, uint32_t sw, uint32_t sh,
                                                    uint32_t* __restrict__ dst, uint32_t dw, uint32_t dh,
                                                    uint32_t flags, uint32_t magnify) {
-  __shared__ float dec[256], enc[256];
+  __shared__ float dec_t[256], enc[256];
   const uint32_t t = threadIdx.y * 16u + threadIdx.x;
-  dec[t] = kSrgbDecode[t];
+  dec_t[t] = kSrgbDecode[t];
   enc[t] = kSrgbThresholds[t];
   __syncthreads();
-  const uint32_t x = blockIdx.x * 16u + threadIdx.x, y = blockIdx.y * 16u + threadIdx.y;
-  if (x >= dw || y >= dh) return;
+  auto dec = [](uint32_t i) { return dec_t[i]; };
+  const uint32_t x = blockIdx.x * 16u + threadIdx.x;
+  if (x >= dw) return;
+  const bool srgb = (flags & 1u) != 0;
   // the quad's varyings (vertex.wgsl:11-13) at this pixel centre, then blit.wgsl:8-9
   const float u = (screen_x(x, dw) + 1.0f) * 0.5f;
-  const float v = 1.0f - (screen_y(y, dh) + 1.0f) * 0.5f;
-  float r, g, b;
-  if (magnify) {  // FilterMode::Linear: 2x2 texels around (u*W - 1/2, v*H - 1/2), clamp to edge
-    const float tu = u * (float)sw - 0.5f, tv = v * (float)sh - 0.5f;
-    const float fu = floorf(tu), fv = floorf(tv);
-    const float a = tu - fu, c = tv - fv;
-    const int iu = (int)fu, iv = (int)fv;
-    const uint32_t x0 = (uint32_t)min(max(iu, 0), (int)sw - 1), x1 = (uint32_t)min(max(iu + 1, 0), (int)sw - 1);
-    const uint32_t y0 = (uint32_t)min(max(iv, 0), (int)sh - 1), y1 = (uint32_t)min(max(iv + 1, 0), (int)sh - 1);
-    const uint32_t t00 = src[y0 * sw + x0], t10 = src[y0 * sw + x1], t01 = src[y1 * sw + x0], t11 = src[y1 * sw + x1];
-    float ch[3];
+  for (uint32_t j = 0; j < kBlitRows; ++j) {
+    const uint32_t y = (blockIdx.y * kBlitRows + j) * 16u + threadIdx.y;
+    if (y >= dh) return;
+    const float v = 1.0f - (screen_y(y, dh) + 1.0f) * 0.5f;
+    float r, g, b;
+    if (magnify) {  // FilterMode::Linear: 2x2 texels around (u*W - 1/2, v*H - 1/2), clamp to edge
+      const float tu = u * (float)sw - 0.5f, tv = v * (float)sh - 0.5f;
+      const float fu = floorf(tu), fv = floorf(tv);
+      const float a = tu - fu, c = tv - fv;
+      const int iu = (int)fu, iv = (int)fv;
+      const uint32_t x0 = (uint32_t)min(max(iu, 0), (int)sw - 1), x1 = (uint32_t)min(max(iu + 1, 0), (int)sw - 1);
+      const uint32_t y0 = (uint32_t)min(max(iv, 0), (int)sh - 1), y1 = (uint32_t)min(max(iv + 1, 0), (int)sh - 1);
+      const uint32_t t00 = src[y0 * sw + x0], t10 = src[y0 * sw + x1], t01 = src[y1 * sw + x0], t11 = src[y1 * sw + x1];
+      float ch[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const uint32_t sh8 = 8u * k;
-      const float top = blit_mix(dec[(t00 >> sh8) & 255u], dec[(t10 >> sh8) & 255u], a);
-      const float bot = blit_mix(dec[(t01 >> sh8) & 255u], dec[(t11 >> sh8) & 255u], a);
-      ch[k] = blit_mix(top, bot, c);
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t sh8 = 8u * k;
+        const float top = blit_mix(dec((t00 >> sh8) & 255u), dec((t10 >> sh8) & 255u), a);
+        const float bot = blit_mix(dec((t01 >> sh8) & 255u), dec((t11 >> sh8) & 255u), a);
+        ch[k] = blit_mix(top, bot, c);
+      }
+      r = ch[0], g = ch[1], b = ch[2];
+    } else {  // FilterMode::Nearest
+      const uint32_t ix = (uint32_t)min(max((int)floorf(u * (float)sw), 0), (int)sw - 1);
+      const uint32_t iy = (uint32_t)min(max((int)floorf(v * (float)sh), 0), (int)sh - 1);
+      const uint32_t tx = src[iy * sw + ix];
+      r = dec(tx & 255u), g = dec((tx >> 8) & 255u), b = dec((tx >> 16) & 255u);
     }
-    r = ch[0], g = ch[1], b = ch[2];
-  } else {  // FilterMode::Nearest
-    const uint32_t ix = (uint32_t)min(max((int)floorf(u * (float)sw), 0), (int)sw - 1);
-    const uint32_t iy = (uint32_t)min(max((int)floorf(v * (float)sh), 0), (int)sh - 1);
-    const uint32_t tx = src[iy * sw + ix];
-    r = dec[tx & 255u], g = dec[(tx >> 8) & 255u], b = dec[(tx >> 16) & 255u];
+    const uint32_t cr = blit_channel(r, srgb, enc), cg = blit_channel(g, srgb, enc), cb = blit_channel(b, srgb, enc);
+    dst[y * dw + x] = (flags & 2u) ? (cb | (cg << 8) | (cr << 16) | (255u << 24)) : (cr | (cg << 8) | (cb << 16) | (255u << 24));
   }
-  const bool srgb = (flags & 1u) != 0;
-  const uint32_t cr = blit_channel(r, srgb, enc), cg = blit_channel(g, srgb, enc), cb = blit_channel(b, srgb, enc);
-  dst[y * dw + x] = (flags & 2u) ? (cb | (cg << 8) | (cr << 16) | (255u << 24)) : (cr | (cg << 8) | (cb << 16) | (255u << 24));
 }
 
 hipError_t launch_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                        uint32_t flags, hipStream_t stream) {
   // mag vs min: texels per output pixel along the more compressed axis (the sampler's LOD)
   const bool magnify = (float)sw / (float)dw <= 1.0f && (float)sh / (float)dh <= 1.0f;
-  hipLaunchKernelGGL(blit_kernel, dim3((dw + 15u) / 16u, (dh + 15u) / 16u), dim3(16, 16), 0, stream,
+  hipLaunchKernelGGL(blit_kernel, dim3((dw + 15u) / 16u, (dh + 16u * kBlitRows - 1u) / (16u * kBlitRows)), dim3(16, 16), 0, stream,
                      (const uint32_t*)src, sw, sh, (uint32_t*)dst, dw, dh, flags, magnify ? 1u : 0u);
   return hipGetLastError();
 }

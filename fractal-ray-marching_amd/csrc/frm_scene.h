@@ -524,12 +524,29 @@ FRM_HD v3 shade_pixel(const FrameUniforms& f, const SceneUniforms& su, uint32_t 
 // Linear colour -> sRGB 8-bit code: the number of thresholds T[1..255] that c reaches.
 // T[k] is the smallest f32 whose exact sRGB encoding rounds to >= k (frm_srgb_table.h),
 // so this equals round(255 * srgb(clamp(c, 0, 1))) exactly; NaN -> 0 (UNORM rule).
+// On the GPU the search is replaced by a candidate code from the sRGB curve evaluated with the
+// hardware log/exp (within one code of the exact code for every f32, tests/test_gpu_present.py
+// checks all of [0, 1] and the special values) and one comparison on each side of it: two
+// table reads instead of eight dependent ones (the table sits in LDS, where data-dependent
+// reads conflict on banks). The table alone decides the code, so the result is the same.
 FRM_HD uint32_t encode_srgb(float c, const float* table) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float cc = __builtin_fminf(__builtin_fmaxf(c, 0.0f), 1.0f);  // NaN -> 0
+  const float s = cc <= 0.0031308f
+                      ? cc * 12.92f
+                      : fmaf(1.055f, __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(cc) * 0.41666666f), -0.055f);
+  const uint32_t k = min((uint32_t)fmaf(s, 255.0f, 0.5f), 254u);
+  const float lo = table[k], hi = table[k + 1u];
+  // table[k + 1] <= c: one up; c < table[k] (then also c < table[k + 1]): one down, except at 0
+  // (NaN stays at 0); branch-free
+  return k + (c >= hi ? 1u : 0u) - ((k > 0u && !(c >= lo)) ? 1u : 0u);
+#else
   uint32_t i = 0;
 #pragma unroll
   for (uint32_t step = 128; step >= 1; step >>= 1)
     if (c >= table[i + step]) i += step;
   return i;
+#endif
 }
 
 FRM_HD uint32_t pack_rgba(v3 c, const float* table) {

@@ -125,7 +125,9 @@ class Renderer:
                # device fast paths (frm_fast.h), each bit-identical to a builtin on its domain
                "sqrt_nosmall": 10, "div_tame": 11, "div_tame_nz": 12, "sin_small": 13,
                "cos_small": 14, "acos_dev": 15, "atan2_tame": 16, "log2_tame": 17,
-               "exp2_tame": 18, "log_posnormal": 19}
+               "exp2_tame": 18, "log_posnormal": 19,
+               # the sRGB store's code (frm_scene.h encode_srgb), as a float
+               "srgb_encode": 20}
 
     def eval_scene(self, points):
         pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)

@@ -246,7 +246,9 @@ enum {
   FRM_MATH_SQRT_NOSMALL = 10, FRM_MATH_DIV_TAME = 11, FRM_MATH_DIV_TAME_NZ = 12,
   FRM_MATH_SIN_SMALL = 13, FRM_MATH_COS_SMALL = 14, FRM_MATH_ACOS_DEV = 15,
   FRM_MATH_ATAN2_TAME = 16, FRM_MATH_LOG2_TAME = 17, FRM_MATH_EXP2_TAME = 18,
-  FRM_MATH_LOG_POSNORMAL = 19
+  FRM_MATH_LOG_POSNORMAL = 19,
+  /* the Rgba8UnormSrgb store's 8-bit code of a linear value (as a float; csrc/frm_scene.h) */
+  FRM_MATH_SRGB_ENCODE = 20
 };
 int frm_eval_scene(frm_ctx* ctx, const float* points, uint32_t n, float* out_distance,
                    float* out_color);
