@@ -64,6 +64,26 @@ __device__ __forceinline__ float div_tame_nz(float a, float b) {
   return fmaf(rem, r, q);
 }
 
+// max_(a, b) for operands that are never signalling NaNs (values computed here): plain v_max_f32,
+// without the quieting canonicalize the compiler puts in front of fmaxf in IEEE mode (same value)
+__device__ __forceinline__ float max_quiet(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// a / b from a precomputed reciprocal r within one ulp of 1 / b: div_tame's two Newton
+// corrections (the same domain: a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40]), with the
+// sign of a zero quotient restored; b > 0 here (the Menger scales), so 0 / b keeps a's sign.
+__device__ __forceinline__ float div_by_rcp(float a, float b, float r) {
+  float q = a * r;
+  float rem = fmaf(-b, q, a);
+  q = fmaf(rem, r, q);
+  rem = fmaf(-b, q, a);
+  q = fmaf(rem, r, q);
+  return (a == 0.0f) ? a : q;
+}
+
 // sincos_ for finite |x| <= 2^22 * pi/2 (the quadrant clamp is a no-op there); negating through
 // the sign bit: (q & 2) ? -v : v == v ^ (bit 1 of q moved to bit 31). Bit-identical.
 // rint(x * 2/pi) by the 1.5 * 2^23 rounding constant: |x * 2/pi| < 2^22, so t = x * 2/pi + K

@@ -32,6 +32,21 @@ void set_menger(SceneUniforms* u, float cross, float factor) {
   u->family = kMenger;
   u->menger_cross = cross;
   u->menger_factor = factor;
+  // Reciprocal scales for the GPU's division (-ci) / scale_i (frm_scene.h de_menger). Its domain
+  // (div_tame's): scale_i in [1, 2^40], and -ci either +-0 or of magnitude in [2^-60, 2^40]. ci
+  // = m - cross with m in [0, 1/2] (a min of maxima of |fract(.) - 1/2|), so |ci| <= 1/2 + cross,
+  // and a non-zero difference of two floats of which one is cross >= 2^-34 is at least
+  // ulp(cross) / 2 >= 2^-60 when m is within a factor of two of cross (Sterbenz: exact) and
+  // larger than cross / 2 otherwise.
+  const uint32_t n = u->n;
+  bool fast = n <= kMengerFastMax && cross >= 0x1p-34f && cross <= 0x1p39f;
+  float scale = 1.0f;
+  for (uint32_t i = 0; fast && i < n; ++i) {
+    if (!(scale >= 1.0f && scale <= 0x1p40f)) fast = false;
+    else u->menger_rcp[i] = (float)(1.0 / (double)scale);
+    scale = scale * factor;
+  }
+  u->menger_fast = fast ? 1u : 0u;
 }
 
 // sierpinski_tetrahedron uniforms, fragment.wgsl:165-178

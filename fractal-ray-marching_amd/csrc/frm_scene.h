@@ -65,11 +65,19 @@ struct Plane {
   v3 anchor, normal;
 };
 
+constexpr uint32_t kMengerFastMax = 16;  // iterations with a precomputed reciprocal scale
+
 struct SceneUniforms {
   uint32_t family;
   uint32_t n;            // parameters.num_iterations
   // Menger (cross_size, scale_factor), fragment.wgsl:21-63
   float menger_cross, menger_factor;
+  // Menger: menger_rcp[i] = RN(1 / scale_i) for the DE's scales (scale_0 = 1, scale_i+1 =
+  // scale_i * factor), set with menger_fast when every division (-ci) / scale_i of the frame lies
+  // in div_tame's domain (frm_host.cpp set_menger): the GPU then divides by Newton steps from
+  // that reciprocal (frm_fast.h div_by_rcp), which give the correctly rounded quotient there
+  uint32_t menger_fast;
+  float menger_rcp[kMengerFastMax];
   // Mandelbulb power = animate_between(4, 9), bailout 100, fragment.wgsl:75
   float mb_power, mb_power_m1, mb_bailout;
   // Sierpinski: TOP.y, HEIGHT*BASE_SCALE_FACTOR*0.5, a/b/c - TOP, fold normals
@@ -120,23 +128,44 @@ FRM_HD float tetrahedron(const SceneUniforms& u, v3 p) {
 }
 
 // menger_sponge(position, cross_size, scale_factor), fragment.wgsl:202-211, with
-// box (138-141), repeat (190-192), cross_inside (194-200).
-template <bool ITERS>
-FRM_HD float de_menger(const SceneUniforms& u, v3 p) {
+// box (138-141), repeat (190-192), cross_inside (194-200). FAST (GPU, u.menger_fast): the
+// division by the scale uses the precomputed reciprocal (the next one is loaded an iteration
+// ahead); same bits.
+template <bool ITERS, bool FAST>
+FRM_HD float menger_folds(const SceneUniforms& u, v3 p, float d) {
   const uint32_t n = iterations<ITERS>(u.n);
-  v3 q = mk(fabsf(p.x) - 0.5f, fabsf(p.y) - 0.5f, fabsf(p.z) - 0.5f);
-  float d = length(max3s(q, 0.0f)) + min_(max_(max_(q.x, q.y), q.z), 0.0f);
   float scale = 1.0f;
+  float rcp = FAST ? u.menger_rcp[0] : 0.0f;
   for (uint32_t i = 0; i < n; ++i) {
+    const float rcp_next = FAST ? u.menger_rcp[i + 1u < kMengerFastMax ? i + 1u : kMengerFastMax - 1u] : 0.0f;
     v3 r = p * scale;
     v3 c = mk(fract_(r.x + 0.5f) - 0.5f, fract_(r.y + 0.5f) - 0.5f, fract_(r.z + 0.5f) - 0.5f);
     v3 a = abs3(c);
     float cx = max_(a.y, a.z), cy = max_(a.z, a.x), cz = max_(a.x, a.y);
     float ci = min_(min_(cx, cy), cz) - u.menger_cross;
-    d = max_(d, (-ci) / scale);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float q = FAST ? div_by_rcp(-ci, scale, rcp) : (-ci) / scale;
+    if constexpr (FAST)
+      d = max_quiet(d, q);
+    else
+      d = max_(d, q);
+#else
+    const float q = (-ci) / scale;
+    d = max_(d, q);
+#endif
     scale = scale * u.menger_factor;
+    rcp = rcp_next;
   }
   return d;
+}
+template <bool ITERS>
+FRM_HD float de_menger(const SceneUniforms& u, v3 p) {
+  v3 q = mk(fabsf(p.x) - 0.5f, fabsf(p.y) - 0.5f, fabsf(p.z) - 0.5f);
+  float d = length(max3s(q, 0.0f)) + min_(max_(max_(q.x, q.y), q.z), 0.0f);
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (u.menger_fast) return menger_folds<ITERS, true>(u, p, d);
+#endif
+  return menger_folds<ITERS, false>(u, p, d);
 }
 
 // sierpinski_tetrahedron(position), fragment.wgsl:164-188. The loop runs i = N-1 .. 0; for
