@@ -40,3 +40,28 @@ def test_num_iterations_above_old_cap(frm_lib, oracle, scene, iters):
         img = r.read_frame()
     ref = oracle.render(p, w, h, 64)
     assert np.array_equal(img, ref["rgba"])
+
+
+def test_pixel_keys_roundtrip_and_injected_orders_keep_bytes(frm_lib, oracle):
+    """The scheduling diagnostics (frm_debug_pixel_keys / frm_debug_set_pixel_keys): the keys the
+    persistent kernel records are 16 log2(bodies + 1) per pixel (0 only where a pixel ran no
+    body); any injected order (reversed, all equal = row-major, random) renders the oracle's bytes
+    and counters; a key map of the wrong size is refused."""
+    w, h = 160, 90
+    p = params_for(18, 12, frm.POWER8_TIME, w, h)
+    ref = oracle.render(p, w, h, 256)
+    with frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL) as r:
+        r.resize(w, h)
+        r.update_parameters_buffer(p)
+        r.render(stats=True)
+        keys = r.pixel_keys()
+        assert keys.shape == (w * h,) and keys.max() > 100
+        rng = np.random.default_rng(3)
+        for inj in (255 - keys, np.zeros_like(keys), rng.integers(0, 256, keys.size).astype(np.uint8)):
+            r.set_pixel_keys(inj)
+            st = r.render(stats=True)
+            assert np.array_equal(r.read_frame(), ref["rgba"])
+            assert st["march_steps"] == int(ref["counters"][2] + ref["counters"][3])
+            assert np.array_equal(r.pixel_keys(), keys)  # the keys a frame records are its own costs
+        with pytest.raises(frm.FrmError):
+            r.set_pixel_keys(keys[:-1])
