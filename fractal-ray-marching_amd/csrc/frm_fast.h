@@ -140,8 +140,10 @@ __device__ __forceinline__ float acos_dev(float t) {
   // rb is used only for |t| > 1/2 (t != 0): t > 0 is t's sign bit, and (t > 0 ? 2s : pi - 2s)
   // == fma(2s, t < 0 ? -1 : 1, t < 0 ? pi : 0), one rounding either way
   const uint32_t tb = __float_as_uint(t);
-  float rb = fma_(2.0f * s, __uint_as_float(bfi_(0x80000000u, tb, 0x3f800000u)),
-                  __uint_as_float((uint32_t)((int32_t)tb >> 31) & __float_as_uint(kPi)));
+  const float sg = __uint_as_float(bfi_(0x80000000u, tb, 0x3f800000u));  // t < 0 ? -1 : 1
+  // the offset (t < 0 ? pi : 0) as fma(sg, -pi/2, pi/2): exact (+0 or pi), one FMA-class
+  // instruction instead of a shift and a mask
+  float rb = fma_(2.0f * s, sg, fma_(sg, -0.5f * kPi, 0.5f * kPi));
 #else
   float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
 #endif
@@ -169,13 +171,15 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
   float r = fma_(a * s, q, a);
 #ifndef FRM_ATAN_SELECT
   // the octant fix-ups without compares: (c ? h - r : r) == fma(r, c ? -1 : 1, c ? h : 0), one
-  // rounding either way (r >= +0). c = sign bit of ax - ay (exact difference: negative iff
-  // ay > ax, +0 when equal) and of x + 0 (-0 + 0 = +0: negative iff x < 0).
+  // rounding either way (r >= +0); the +-1 is a bit-field insert of c's sign bit into 1.0.
+  // c = sign bit of ax - ay (exact difference: negative iff ay > ax, +0 when equal) and of
+  // x + 0 (-0 + 0 = +0: negative iff x < 0).
   const uint32_t c1 = __float_as_uint(ax - ay), c2 = __float_as_uint(x + 0.0f);
-  r = fma_(r, __uint_as_float(bfi_(0x80000000u, c1, 0x3f800000u)),
-           __uint_as_float((uint32_t)((int32_t)c1 >> 31) & __float_as_uint(kHalfPi)));
-  r = fma_(r, __uint_as_float(bfi_(0x80000000u, c2, 0x3f800000u)),
-           __uint_as_float((uint32_t)((int32_t)c2 >> 31) & __float_as_uint(kPi)));
+  const float s1 = __uint_as_float(bfi_(0x80000000u, c1, 0x3f800000u));
+  const float s2 = __uint_as_float(bfi_(0x80000000u, c2, 0x3f800000u));
+  // offsets (c ? h : 0) as fma(s, -h/2, h/2): exact (+0 or h)
+  r = fma_(r, s1, fma_(s1, -0.5f * kHalfPi, 0.5f * kHalfPi));
+  r = fma_(r, s2, fma_(s2, -0.5f * kPi, 0.5f * kPi));
 #else
   r = (ay > ax) ? kHalfPi - r : r;
   r = (x < 0.0f) ? kPi - r : r;
