@@ -95,6 +95,13 @@ __device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) 
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
   return r;
 }
+// v ^ (m & 0x80000000) in one v_bitop3_b32 (truth table 0x6c: (src0 & src2) ^ src1); left to
+// itself the compiler sometimes splits it into v_and + v_xor
+__device__ __forceinline__ uint32_t xor_sign_(uint32_t v, uint32_t m) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(r) : "v"(m), "v"(v), "s"(0x80000000u));
+  return r;
+}
 __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
 #ifdef FRM_FAST_V1
   float j = rintf(x * kTwoOverPi);
@@ -121,8 +128,8 @@ __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out
   const float sv = __uint_as_float(bfi_(odd, __float_as_uint(c), __float_as_uint(s)));
   const float cv = __uint_as_float(bfi_(odd, __float_as_uint(s), __float_as_uint(c)));
 #endif
-  *s_out = __uint_as_float(__float_as_uint(sv) ^ ((q << 30) & 0x80000000u));
-  *c_out = __uint_as_float(__float_as_uint(cv) ^ (((q + 1u) << 30) & 0x80000000u));
+  *s_out = __uint_as_float(xor_sign_(__float_as_uint(sv), q << 30));
+  *c_out = __uint_as_float(xor_sign_(__float_as_uint(cv), (q + 1u) << 30));
 }
 
 // acos_ with the exact-for-its-range sqrt (zb is 0 or >= 2^-25 for |t| <= 1; NaN/negative
