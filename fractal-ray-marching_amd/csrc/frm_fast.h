@@ -154,7 +154,8 @@ __device__ __forceinline__ float acos_dev(float t) {
 #else
   float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
 #endif
-  float rs = kHalfPi - copysignf(s, t);
+  // pi/2 - copysign(s, t) == fma(-sg, s, pi/2): sg * s is exact (+-s; t = -0 gives sg = -1)
+  float rs = fma_(-sg, s, kHalfPi);
   return big ? rb : rs;
 }
 
