@@ -34,9 +34,7 @@ namespace frm {
 template <bool ITERS>
 FRM_HD uint32_t iterations(uint32_t n) {
   if (!ITERS) return 0u;
-#ifndef FRM_CANARY_NO_ITERS_ASSUME  // the compiler canary (tests/test_gpu_compiler_canary.py) builds without it
   FRM_ASSUME(n >= 1u);
-#endif
   return n;
 }
 
