@@ -13,7 +13,7 @@ import os
 import sys
 
 import numpy as np
-from scipy.ndimage import maximum_filter
+from scipy.ndimage import maximum_filter, uniform_filter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "fractal-ray-marching_amd")]
@@ -43,13 +43,35 @@ def spikes(src, thr, pad, boost=255):
     return np.where(hi, np.maximum(upsample(src, 1), boost), upsample(src, 1))
 
 
+def local_sd(src, size=9):
+    """standard deviation of the source keys over a size x size window (noisy regions)"""
+    f = src.astype(np.float32)
+    m = uniform_filter(f, size)
+    return np.sqrt(np.maximum(uniform_filter(f * f, size) - m * m, 0.0))
+
+
+def noisy(src, pad, alpha, size=9):
+    """max over +-pad, raised by alpha x the local standard deviation of the source keys"""
+    up = upsample(src, pad).astype(np.float32)
+    sd = upsample(local_sd(src, size), 0)
+    return np.clip(up + alpha * sd, 0, 255)
+
+
 RESAMPLERS = {
     "max1": lambda s: upsample(s, 1),
     "max4": lambda s: upsample(s, 4),
+    "max8": lambda s: upsample(s, 8),
     "max16": lambda s: upsample(s, 16),
     "spk190p16": lambda s: spikes(s, 190, 16),
     "spk185p8": lambda s: spikes(s, 185, 8),
+    "max4sd1": lambda s: noisy(s, 4, 1.0),
+    "max4sd2": lambda s: noisy(s, 4, 2.0),
+    "max8sd2": lambda s: noisy(s, 8, 2.0),
+    "max8sd4": lambda s: noisy(s, 8, 4.0),
+    "max1sd3": lambda s: noisy(s, 1, 3.0),
 }
+if os.environ.get("RESAMPLERS"):
+    RESAMPLERS = {k: RESAMPLERS[k] for k in os.environ["RESAMPLERS"].split(",")}
 
 res = {"ms": {}}
 with frm.Renderer(device=0, max_steps=w.max_steps) as r:
