@@ -273,8 +273,17 @@ def main():
     # costliest pixels' sequential marches) is paid once per batch (measured, DESIGN.md sections
     # 6-7: 8-way rank share 1.67 ms/frame at 1 frame per launch and 3 in flight -> 1.38-1.44 at
     # 8 per launch and 2 in flight; whole 4K frame 11.20 -> 10.84 ms at 8 per launch, 1080p
-    # 3.12 -> 2.80). Animated workloads change the scene every frame: one frame per launch.
-    batch = 1 if w.animated else max(1, min(args.batch or 8, frm.FRM_MAX_BATCH))
+    # 3.12 -> 2.80; 16 per launch: 10.42 -> 10.37 ms, 1080p 2.66 -> 2.63, 8-way share 1.416 ->
+    # 1.385-1.402, profiles/round2/batch32/). Auto: the timed frames in equal launches of at
+    # most 16 (20 frames: 2 x 10). Animated workloads change the scene every frame: one frame
+    # per launch.
+    if w.animated:
+        batch = 1
+    elif args.batch:
+        batch = max(1, min(args.batch, frm.FRM_MAX_BATCH))
+    else:
+        k = max(1, args.steps)
+        batch = -(-k // -(-k // 16))
     if args.inflight:
         inflight = args.inflight
     elif batch > 1:
@@ -282,9 +291,8 @@ def main():
     else:
         inflight = 3 if split > 1 or local_pixels < 4_000_000 else 2
     inflight = max(1, min(inflight, frm.FRM_MAX_FRAMES_IN_FLIGHT))
-    # whole batches: timed and warmup frame counts rounded up to multiples of the batch
-    args.steps = -(-args.steps // batch) * batch
-    args.warmup = -(-args.warmup // batch) * batch
+    # exactly --steps timed and --warmup untimed frames: launches of `batch` frames, the last one
+    # of each run takes the remainder (RowTiledFrame.run)
     r = frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=inflight)
     r.resize(w.width, w.height)
     r.update_parameters_buffer(params)
@@ -303,14 +311,14 @@ def main():
     kev = []  # (start, stop) HIP events around every render launch of the timed region
     timing = {"on": False}
 
-    def render_bands(buf, br, first, stride, slot):
+    def render_bands(buf, br, first, stride, slot, count):
         s = streams[slot]
         ev = None
         if timing["on"]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(s)
-        if batch > 1:  # one launch, `batch` frames (same scene and camera here), frame b at b * tf.nbytes
-            r.render_bands_batch([params] * batch, buf.data_ptr(), tf.nbytes, br, first, stride, s.cuda_stream,
+        if batch > 1:  # one launch, `count` frames (same scene and camera here), frame b at b * tf.nbytes
+            r.render_bands_batch([params] * count, buf.data_ptr(), tf.nbytes, br, first, stride, s.cuda_stream,
                                  counters.data_ptr())
         else:
             r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())

@@ -215,6 +215,14 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
     const bool whole = a.g.first_band == 0 && a.g.band_stride == 1 && npix == a.f.width * a.f.height;
     const bool same = sl.sched_history && key == sl.sched_key;
     const bool rescale = !same && sl.sched_history && sl.sched_whole && whole;
+    // a slot without history of this geometry takes another slot's keys: with frames in
+    // flight, every slot's first launch would otherwise fetch in row-major order
+    int donor = -1;
+    if (!same && !rescale)
+      for (uint32_t j = 0; j < ctx->nslots && donor < 0; ++j) {
+        const Slot& o = ctx->slots[j];
+        if (j != si && o.sched_history && o.sched_key == key && o.sched_cap >= npix) donor = (int)j;
+      }
     if (npix > sl.sched_cap) {
       int rc = wait_slot(ctx, sl);
       if (rc) return rc;
@@ -244,7 +252,12 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       FRM_HIP(ctx, rescale_keys(sl.sched_keys, sl.sched_w, sl.sched_h, tmp, a.f.width, a.f.height, s));
       FRM_HIP(ctx, hipMemcpyAsync(sl.sched_keys, tmp, npix, hipMemcpyDeviceToDevice, s));
     }
-    const bool history = same || rescale;
+    if (donor >= 0) {  // keys order fetches only, never a pixel's bytes
+      Slot& dn = ctx->slots[donor];
+      if (dn.pending && dn.last_stream != s) FRM_HIP(ctx, hipStreamWaitEvent(s, dn.done, 0));
+      FRM_HIP(ctx, hipMemcpyAsync(sl.sched_keys, dn.sched_keys, npix, hipMemcpyDeviceToDevice, s));
+    }
+    const bool history = same || rescale || donor >= 0;
     FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
                                  sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
     a.pixel_order = sl.sched_order;

@@ -9,7 +9,7 @@
 #include "frm_uniforms.h"
 
 namespace frm {
-constexpr uint32_t kMaxBatch = 8;  // FRM_MAX_BATCH: frames per multi-frame launch
+constexpr uint32_t kMaxBatch = FRM_MAX_BATCH;  // frames per multi-frame launch
 
 // Row-band geometry of one launch: local row lr lives in band (lr / band_rows) of this
 // launch; that band is global band first_band + (lr / band_rows) * band_stride.

@@ -23,7 +23,7 @@ FRM_ERR_COMPILE = 8
 
 FRM_NUM_SCENES = 19
 FRM_MAX_FRAMES_IN_FLIGHT = 8
-FRM_MAX_BATCH = 8
+FRM_MAX_BATCH = 32
 FRM_DEFAULT_MAX_STEPS = 5000
 FRM_MAX_STEPS_LIMIT = 4194303
 FRM_MAX_NUM_ITERATIONS = 0xFFFFFFFF

@@ -20,19 +20,21 @@ from . import tiling
 class RowTiledFrame:
     def __init__(self, width, height, rank, world, band_rows, device, render_bands, unshuffle,
                  group=None, inflight=1, streams=None, collective=None, stage_host=None, batch=1):
-        """render_bands(buf, band_rows, first_band, band_stride, slot): enqueue the render of
-        this rank's bands into the uint8 tensor buf (device memory for the GPU path) for
-        frame slot `slot` (k % inflight; the GPU path renders it on streams[slot]).
+        """render_bands(buf, band_rows, first_band, band_stride, slot, count): enqueue the
+        render of this rank's bands of the next `count` frames (1 <= count <= batch) into the
+        uint8 tensor buf (device memory for the GPU path), frame b at b * nbytes, for launch
+        slot `slot` (k % inflight; the GPU path renders it on streams[slot]).
         unshuffle(gathered, frame, slot): rank 0 only; rank-major band buffers -> row-major
         frame. inflight = frames in flight: frame k's render, gather and unshuffle are
         enqueued on streams[k % inflight] (torch streams; None = the current stream, as in
         the CPU tests), so up to `inflight` frames overlap on the GPU. collective: gather
         through torch.distributed (default: when world > 1; True with world 1 runs the
         same gather/unshuffle path on one rank, a test hook for RCCL on one GPU).
-        batch: frames per launch (frm_render_bands_batch): render_bands(buf, ...) renders the
-        next `batch` frames into buf, frame b at b * nbytes, one frame's bands each; one gather
-        moves them all; unshuffle(gathered, rank_stride, frame, slot) rebuilds one frame from
-        rank-major buffers rank_stride bytes apart.
+        batch: frames per launch (frm_render_bands_batch): a launch renders up to `batch`
+        frames (run(n) issues n // batch full launches and one launch of the remainder, so
+        exactly n frames are rendered), one frame's bands each; one gather moves them all;
+        unshuffle(gathered, rank_stride, frame, slot) rebuilds one frame from rank-major
+        buffers rank_stride bytes apart.
         stage_host: gather through host copies of the band buffers (default: when the
         backend is gloo and the buffers live on a GPU). A test hook: RCCL refuses two ranks
         on one GPU, so a 1-GPU box runs the row split with gloo, whose gather takes host
@@ -70,34 +72,35 @@ class RowTiledFrame:
                            for _ in range(nbuf)]
         self.frames_done = 0
         self.last = 0
+        self.last_count = 1
 
     def _stream(self, k):
         if self.streams is None:
             return contextlib.nullcontext()
         return torch.cuda.stream(self.streams[k % self.inflight])
 
-    def _issue(self, k):
+    def _issue(self, k, count):
         buf = self.bufs[k % self.nbuf]
         with self._stream(k):
-            self.render_bands(buf, self.band_rows, self.rank, self.world, k % self.inflight)
+            self.render_bands(buf, self.band_rows, self.rank, self.world, k % self.inflight, count)
             if not self.collective:
                 return None
             glist = None
             g = self.gathered[k % self.nbuf] if self.rank == 0 else None
+            n = count * self.nbytes  # this launch's frames, rank-major: rank i's at i * n
             if self.stage_host:
-                host = buf.cpu()  # waits for this frame's render on the stream
+                host = buf[:n].cpu()  # waits for this launch's render on the stream
                 if self.rank == 0:
                     glist = [torch.empty_like(host) for _ in range(self.world)]
                 dist.gather(host, gather_list=glist, dst=0, group=self.group)
                 if self.rank == 0:
-                    g.copy_(torch.cat(glist))
+                    g[:self.world * n].copy_(torch.cat(glist))
                 return None
             if self.rank == 0:
-                n = self.batch * self.nbytes
                 glist = [g[i * n:(i + 1) * n] for i in range(self.world)]
-            return dist.gather(buf, gather_list=glist, dst=0, group=self.group, async_op=True)
+            return dist.gather(buf[:n], gather_list=glist, dst=0, group=self.group, async_op=True)
 
-    def _finish(self, k, work):
+    def _finish(self, k, work, count):
         if self.collective:
             with self._stream(k):
                 if work is not None:
@@ -105,34 +108,37 @@ class RowTiledFrame:
                 if self.rank == 0:
                     g, fr = self.gathered[k % self.nbuf], self.frames[k % self.nbuf]
                     fb = self.height * self.width * 4
-                    for b in range(self.batch):  # frame b of the batch: rank r's at r*B*nbytes + b*nbytes
-                        self.unshuffle(g[b * self.nbytes:], self.batch * self.nbytes, fr[b * fb:(b + 1) * fb],
+                    for b in range(count):  # frame b of the launch: rank r's at r*count*nbytes + b*nbytes
+                        self.unshuffle(g[b * self.nbytes:], count * self.nbytes, fr[b * fb:(b + 1) * fb],
                                        k % self.inflight)
         self.last = k % self.nbuf
-        self.frames_done += self.batch
+        self.last_count = count
+        self.frames_done += count
 
     def run(self, n, before_frame=None):
         """Render, gather and reassemble n frames (asynchronous on the GPU path: callers
-        synchronize the device to wait for the last one; n a multiple of batch).
-        before_frame(k), if given, runs on the host before frame k is issued (e.g. to advance
-        animated parameters); for a batch, before each of its frames, before the launch."""
-        if n % self.batch:
-            raise ValueError(f"{n} frames is not a multiple of the batch ({self.batch})")
+        synchronize the device to wait for the last one). Launches take `batch` frames each,
+        the last one the remainder. before_frame(k), if given, runs on the host before frame k
+        is issued (e.g. to advance animated parameters); for a launch of several frames, before
+        each of its frames, before the launch."""
         pending = None
-        for k in range(n // self.batch):
+        done = 0
+        for k in range(-(-n // self.batch)):
+            count = min(self.batch, n - done)
             if before_frame is not None:
-                for j in range(self.batch):
-                    before_frame(k * self.batch + j)
-            work = self._issue(k)
+                for j in range(count):
+                    before_frame(done + j)
+            done += count
+            work = self._issue(k, count)
             if pending is not None:
                 self._finish(*pending)
-            pending = (k, work)
+            pending = (k, work, count)
         if pending is not None:
             self._finish(*pending)
 
     def output(self):
         """Rank 0: the last frame, flat RGBA8 (the band buffer itself when world == 1)."""
         if not self.collective:
-            return self.bufs[self.last][(self.batch - 1) * self.nbytes:]
+            return self.bufs[self.last][(self.last_count - 1) * self.nbytes:self.last_count * self.nbytes]
         fb = self.height * self.width * 4
-        return self.frames[self.last][(self.batch - 1) * fb:]
+        return self.frames[self.last][(self.last_count - 1) * fb:self.last_count * fb]

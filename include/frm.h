@@ -218,7 +218,7 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
  * num_iterations, time-derived scene constants and aspect as params[0]
  * (FRM_ERR_INVALID_ARGUMENT otherwise). The context's parameters become params[count-1].
  * Counters are added over all frames. Bytes per frame are those of frm_render_bands. */
-#define FRM_MAX_BATCH 8u
+#define FRM_MAX_BATCH 32u
 int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* params,
                            uint8_t* dev_dst, size_t frame_stride_bytes, uint32_t band_rows,
                            uint32_t first_band, uint32_t band_stride, void* stream,

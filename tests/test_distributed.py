@@ -45,12 +45,12 @@ def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None, ba
     def before_frame(k):
         state["ps"].append(params_for(18, 8, _times()[k], W, H))
 
-    def render_bands(buf, br, first, stride, slot):
-        assert 0 <= slot < inflight
+    def render_bands(buf, br, first, stride, slot, count):
+        assert 0 <= slot < inflight and 1 <= count <= batch
         rows = tiling.global_rows(H, br, first, stride)
         valid = [y for y in rows if y >= 0]
         nb = len(rows) and tiling.rank_buffer_rows(H, br, stride) * W * 4
-        for b, p in enumerate(state["ps"][-batch:]):  # the batch's frames, in order
+        for b, p in enumerate(state["ps"][-count:]):  # the launch's frames, in order
             r = frm_oracle.render(p, W, H, 128, rows=valid, threads=2)
             out = buf.numpy()[b * nb:(b + 1) * nb].reshape(-1, W, 4)
             out[:len(valid)] = r["rgba"]  # padding rows (y < 0) are only at the end
@@ -77,10 +77,12 @@ def _worker(rank, world, port, W, H, band_rows, inflight, q, stage_host=None, ba
 
 @pytest.mark.parametrize("W,H,band_rows,inflight,stage_host,batch", [
     (48, 27, 4, 1, None, 1), (40, 24, 6, 1, None, 1), (48, 27, 4, 2, None, 1), (40, 24, 6, 3, None, 1),
-    (40, 24, 6, 3, True, 1), (48, 27, 4, 1, None, 3), (40, 24, 6, 2, True, 3)])
+    (40, 24, 6, 3, True, 1), (48, 27, 4, 1, None, 3), (40, 24, 6, 2, True, 3), (48, 27, 4, 2, None, 2),
+    (40, 24, 6, 1, True, 2)])
 def test_two_rank_gather_equals_single_frame(oracle, W, H, band_rows, inflight, stage_host, batch):
     """stage_host=True: the host-staged gather bench.py uses for gloo ranks on one GPU;
-    batch=3: the three frames rendered by one multi-frame launch per rank, one gather."""
+    batch=3: the three frames rendered by one multi-frame launch per rank, one gather;
+    batch=2: a launch of two frames, then one of the remaining frame (exact frame counts)."""
     from helpers import params_for
     import frm
 

@@ -88,3 +88,30 @@ def test_batch_rejects_frames_that_differ_beyond_the_camera(frm_lib):
             assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
         with pytest.raises(frm.FrmError):
             r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), w * h * 4, h, 0, 1)
+
+
+def test_batch_of_max_frames_two_slots(frm_lib, oracle):
+    """FRM_MAX_BATCH frames per launch (the cameras cycling over four poses), two frames in
+    flight: the second slot's first launch fetches by the keys the first slot recorded
+    (history shared between slots); every frame of both launches equals the oracle's."""
+    import torch
+
+    w, h = 64, 36
+    poses = _poses(18, 12, frm.POWER8_TIME, w, h)
+    refs = [oracle.render(p, w, h, 256) for p in poses]
+    B = frm.FRM_MAX_BATCH
+    ps = [poses[k % len(poses)] for k in range(B)]
+    fb = w * h * 4
+    dev = torch.device("cuda", 0)
+    outs = [torch.zeros(B * fb, dtype=torch.uint8, device=dev) for _ in range(2)]
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    with frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL, frames_in_flight=2) as r:
+        r.resize(w, h)
+        for rep in range(3):
+            for o in outs:
+                r.render_bands_batch(ps, o.data_ptr(), fb, h, 0, 1, 0, counters.data_ptr())
+            torch.cuda.synchronize()
+            for j, o in enumerate(outs):
+                img = o.cpu().numpy().reshape(B, h, w, 4)
+                for k in range(B):
+                    assert np.array_equal(img[k], refs[k % len(refs)]["rgba"]), f"rep {rep} launch {j} frame {k}"

@@ -110,7 +110,8 @@ def test_rccl_gather_pipeline_one_rank(frm_lib, refs):
                           frames_in_flight=F) as r:
             r.resize(W, H)
 
-            def render_bands(buf, br, first, stride, slot):
+            def render_bands(buf, br, first, stride, slot, count):
+                assert count == 1
                 r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, streams[slot].cuda_stream,
                                counters.data_ptr())
 
