@@ -5,7 +5,7 @@
 set -o pipefail
 OUT=${OUT:-gpurun_out/r2pmc}
 mkdir -p "$OUT"
-for spec in "HEADLINE:--steps 16 --warmup 8" "C2:--steps 16 --warmup 8" "C3:--steps 16 --warmup 8" "C4:--steps 12 --warmup 8" "C5:--steps 3 --warmup 2"; do
+for spec in "HEADLINE:--batch 16 --steps 32 --warmup 32" "C2:--batch 16 --steps 32 --warmup 32" "C3:--batch 16 --steps 32 --warmup 32" "C4:--batch 16 --steps 32 --warmup 32" "C5:--steps 3 --warmup 2"; do
   wl=${spec%%:*}; a=${spec#*:}
   OUT=$OUT/$wl ARGS="--workload $wl $a --no-cpu-baseline" bash tools/pmc.sh > /dev/null || { echo "pmc $wl failed"; exit 1; }
   python tools/pmc_summary.py $OUT/$wl march_persistent > $OUT/pmc_${wl}_march.json || exit 1
