@@ -26,6 +26,9 @@ static constexpr uint32_t kDefaultServiceMin = 24;  // swept 16..36 on MI355X (r
 // and the persistent kernel's fixed costs (pixel sort, grid, separate shading pass) outweigh
 // its load balancing: 256x256 runs 23 G steps/s simple vs 10 persistent, 1920x1080 8 vs 20.
 static constexpr uint64_t kSimplePixelsPerCu = 1536;
+// Queue positions a launch may claim beyond its pixels (2 chunks per wave of a grid of up to
+// 2^17 waves); launches are limited to 2^32 - 1 - this many fetch positions.
+static constexpr uint64_t kQueueHeadroom = 1ull << 24;
 
 // One frame in flight: the device state a render launch owns until it completes. A context
 // has config.frames_in_flight slots and launches round-robin over them, so frame k+1 can
@@ -554,7 +557,9 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
   if (frame_stride_bytes < need || frame_stride_bytes % 4u)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "frame stride %zu: below a frame's %zu bytes or not a multiple of 4",
                 frame_stride_bytes, need);
-  if ((uint64_t)rows * ctx->width * count >= 0xFFFFFFFFull)
+  // fetch positions are u32 and every wave's last queue claims run up to two chunks past the
+  // end (kQueueHeadroom covers any persistent grid): keep them from wrapping
+  if ((uint64_t)rows * ctx->width * count >= 0xFFFFFFFFull - kQueueHeadroom)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "batch of %u frames of %u x %u local pixels too large", count,
                 ctx->width, rows);
   // frames of one launch may differ in camera only: same scene uniforms (scene, iterations,

@@ -11,7 +11,9 @@ timeout -k 10 400 python bench.py > "$OUT/bench_HEADLINE.json" 2> "$OUT/bench.er
 python -c "import json;d=json.load(open('$OUT/bench_HEADLINE.json'));print('HEADLINE', round(d['value'],3), 'G/s', round(d['ms_per_step'],3), 'ms frac', round(d['roofline']['frac'],4), 'valu_busy', d['roofline'].get('valu_busy'), 'sha_ok', d['frame_sha_ok'], 'cpu', d['cpu_baseline']['value'])"
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { echo "rocprof failed"; tail -20 "$OUT/prof.err"; exit 1; }
-python tools/rocprof_timed.py $(find "$OUT/prof" -name "*kernel_trace.csv" | head -1) 4 8 > "$OUT/rocprof_timed_HEADLINE.txt" && tail -n 3 "$OUT/rocprof_timed_HEADLINE.txt"
+# the profiled run's timed launches: steps / frames_per_launch of them, that many frames each
+read K B < <(python -c "import json;d=json.load(open('$OUT/prof_bench.json'));b=d['config']['frames_per_launch'];print(-(-d['steps']//b), b)")
+python tools/rocprof_timed.py $(find "$OUT/prof" -name "*kernel_trace.csv" | head -1) $K $B > "$OUT/rocprof_timed_HEADLINE.txt" && tail -n 3 "$OUT/rocprof_timed_HEADLINE.txt"
 cp $(find "$OUT/prof" -name "*kernel_stats.csv" | head -1) "$OUT/rocprof_kernel_stats_HEADLINE.csv"
 for spec in "C1:" "C2:" "C3:" "C4:" "C5:--steps 2 --warmup 1"; do
   wl=${spec%%:*}; a=${spec#*:}
