@@ -24,7 +24,7 @@ process (before anything touches a GPU) and prints rank 0's line:
 Prints ONE JSON line on rank 0. `value` = G ray-march-steps/s of the whole job
 (primary + shadow march() iterations, counted exactly by the kernel, / wall time).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload HEADLINE|C2|C3|C4|C5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload HEADLINE|HEADLINE_FLY|C2|C3|C4|C5]
                     [--pose P0|P1|P2] [--kernel persistent|simple] [--no-cpu-baseline]
 """
 import argparse
@@ -81,6 +81,7 @@ def parse():
                     "queue, so a launch's tail is paid once per batch); 0 = auto (DESIGN.md section 7); "
                     "animated workloads (a new time every frame) always 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in loop measurement (dropin_ms_per_frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
                     "copy of csrc/ (frm_reload, hiprtc)")
@@ -137,21 +138,22 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 
 def pmc_summary(workload, world):
-    """Hardware counters of the dominant kernel (march_persistent) from the committed
-    rocprofv3 --pmc passes of this workload (tools/pmc.sh + tools/pmc_summary.py: one
-    counter group per pass; FETCH_SIZE doubled and KiB -> B per MI355X_MICROARCH.md).
+    """Hardware counters of the render kernels from the committed rocprofv3 --pmc passes of
+    this workload (tools/pmc.sh + tools/pmc_summary.py: one counter group per pass; FETCH_SIZE
+    doubled and KiB -> B per MI355X_MICROARCH.md): march_persistent (the dominant kernel:
+    VALU busy, lane utilisation, HBM bytes) and shade_pass (HBM bytes). N > 1: the summary of
+    one rank's share of the row split (pmc_<workload>_share<N>_*.json) when committed.
     PMC collection needs its own profiler passes (they serialise the kernels), so bench.py
     reports the committed measurement and names it, newest round first, and only when the
     summary's recorded source hash equals the hash of the kernel sources being run
     (frm.provenance): counters of an older kernel are reported as stale, never as current."""
     from frm import provenance
 
-    if world != 1:
-        return None
     cur = provenance.source_sha256()
     stale = None
-    for rnd in ("round2", "round1"):
-        path = os.path.join(ROOT, "profiles", rnd, f"pmc_{workload}_march.json")
+    tag = workload if world == 1 else f"{workload}_share{world}"
+    for rnd in ("round3", "round2", "round1"):
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_march.json")
         if not os.path.exists(path):
             continue
         with open(path) as fh:
@@ -160,17 +162,58 @@ def pmc_summary(workload, world):
             stale = stale or os.path.relpath(path, ROOT)
             continue
         B = s.get("frames_per_dispatch", 1)
+        march = (s["hbm_read_bytes"] + s["hbm_write_bytes"]) / B
+        shade = shade_src = None
+        spath = path.replace("_march.json", "_shade.json")
+        if os.path.exists(spath):
+            with open(spath) as fh:
+                sh = json.load(fh)
+            if sh.get("source_sha256") == cur:
+                shade = (sh["hbm_read_bytes"] + sh["hbm_write_bytes"]) / sh.get("frames_per_dispatch", 1)
+                shade_src = os.path.relpath(spath, ROOT)
         return {
-            # HBM bytes per frame of the dominant kernel (a dispatch renders B frames)
-            "traffic": (s["hbm_read_bytes"] + s["hbm_write_bytes"]) / B,
+            # HBM bytes per frame (a dispatch renders B frames): march + shade, and the split
+            "traffic": march + (shade or 0.0),
+            "traffic_split": {"march_persistent": march, "shade_pass": shade},
             "valu_busy": s["valu_busy"],
             "valu_lane_utilization": s["valu_lane_utilization"],
             "hbm_write_gbps": s["hbm_write_gbps"],
             "hbm_write_frac": s["hbm_write_gbps"] / HBM_PEAK_GBPS,
-            "source": os.path.relpath(path, ROOT),
+            "source": os.path.relpath(path, ROOT) + (f" + {shade_src}" if shade_src else ""),
             "source_sha256": cur,
         }
     return {"stale": stale, "source_sha256": cur} if stale else None
+
+
+def dropin_loop(frm, torch, w, args, flags, local, camera):
+    """The drop-in binding's frame loop, measured in the same run:
+    a context with frames_in_flight = 1, one frm_render per frame with that frame's
+    Parameters (frm.frame_sequence, as bench's timed region), and the host waiting for every
+    frame before the next (frm_render with stats: the reference presents every frame,
+    graphics.rs:91-110). Untimed: 2 frames of frame 0. Timed: min(--steps, 20) frames."""
+    seq = frm.frame_sequence(w, pose=args.pose, camera=camera)
+    p0 = next(seq)
+    n = max(1, min(args.steps, 20))
+    with frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=1) as r:
+        r.resize(w.width, w.height)
+        r.update_parameters_buffer(p0)
+        for _ in range(2):
+            r.render(stats=True)
+        steps = 0
+        kernel_ms = 0.0
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            if k > 0 and w.animated:
+                r.update_parameters_buffer(next(seq))
+            st = r.render(stats=True)
+            steps += st["march_steps"]
+            kernel_ms += st["kernel_ms"]
+        dt = time.perf_counter() - t0
+    return {"dropin_ms_per_frame": dt / n * 1e3,
+            "dropin": {"frames": n, "value": steps / dt / 1e9, "unit": "Gray-march-steps/s",
+                       "kernel_ms_per_frame": kernel_ms / n, "frames_in_flight": 1, "frames_per_launch": 1,
+                       "loop": "frm_render(stats) per frame, host waits for each frame (INTEGRATION.md section 3)"}}
 
 
 def launch_ranks(args):
@@ -199,16 +242,27 @@ def launch_ranks(args):
 GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
 
-def frame_check(frame, workload, pose, animated):
-    """sha256 of the last rendered (for N>1: gathered and reassembled) frame against the
-    oracle's whole-frame golden hash (tests/golden/fullsize.json, generated on the CPU by
-    tests/golden/make_fullsize_golden.py): the output does not depend on how the frame was
-    tiled over ranks or scheduled. None when no golden frame exists for this configuration
-    (other poses; animated workloads, whose last frame's time depends on the frame count)."""
+def golden_key(workload, pose):
+    """The golden frame that equals frame 0 of the timed sequence (frm.frame_sequence): the
+    fixed frame itself; C5's first animation time; the fly-through's frame 0 is the headline."""
+    if workload == "C5":
+        return f"C5_{pose}_t0"
+    if workload == "HEADLINE_FLY":
+        return f"HEADLINE_{pose}"
+    return f"{workload}_{pose}"
+
+
+def frame_check(frame, workload, pose):
+    """sha256 of the first timed frame (for N>1: gathered and reassembled; kept by
+    RowTiledFrame.run(capture=...)) against the oracle's whole-frame golden hash
+    (tests/golden/fullsize.json, generated on the CPU by tests/golden/make_fullsize_golden.py):
+    the output does not depend on how the frame was tiled over ranks or scheduled. Timed frame
+    0 is frame 0 of the workload's frame sequence (animated workloads too: the warmup renders
+    frame 0, the timed region frames 0..K-1). None when no golden frame exists."""
     sha = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
-    key = f"{workload}_{pose}"
+    key = golden_key(workload, pose)
     gold = None
-    if not animated and os.path.exists(GOLDEN):
+    if os.path.exists(GOLDEN):
         with open(GOLDEN) as fh:
             gold = json.load(fh).get(key)
     return {"frame_sha256": sha, "frame_sha_ok": None if gold is None else sha == gold["sha256"],
@@ -251,16 +305,22 @@ def main():
         comm_ranks = dist.get_world_size()
 
     w = frm.WORKLOADS[args.workload]
-    params = frm.make_parameters(w, pose=args.pose)
     afr = world > 1 and args.split == "frames"
+    camera = None
     if afr and rank > 0:
         # alternate-frame rendering: rank r renders the view of the same workload from the
         # pose rotated about +y by r * pi/4 (an orbit fly-through, looking at the same
         # point as the base pose; rank 0 renders the base pose itself)
         (x, y, z), yaw, pitch = frm.POSES[args.pose]
         a = rank * math.pi / 4
-        cam = frm.Camera((math.cos(a) * x + math.sin(a) * z, y, -math.sin(a) * x + math.cos(a) * z), yaw + a, pitch)
-        params.update_camera(cam)
+        camera = ((math.cos(a) * x + math.sin(a) * z, y, -math.sin(a) * x + math.cos(a) * z), yaw + a, pitch)
+    # Frame k of the timed region renders frame k of the workload's frame sequence
+    # (frm.frame_sequence: the reference's InitializedApp::update, initialized_app.rs:43-48;
+    # fixed workloads repeat frame 0, animated ones advance time by 1/60 s per frame, the
+    # fly-through also orbits the camera). The warmup renders frame 0.
+    seq = frm.frame_sequence(w, pose=args.pose, camera=camera)
+    params = next(seq)
+    frame0 = params
     flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
         {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel])
     split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
@@ -319,7 +379,7 @@ def main():
             ev[0].record(s)
         if batch > 1:  # one launch, `count` frames (same scene and camera here), frame b at b * tf.nbytes
             r.render_bands_batch([params] * count, buf.data_ptr(), tf.nbytes, br, first, stride, s.cuda_stream,
-                                 counters.data_ptr())
+                                 counters.data_ptr(), dst_bytes=buf.numel())
         else:
             r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
         if ev is not None:
@@ -333,20 +393,14 @@ def main():
     tf = RowTiledFrame(w.width, w.height, 0 if split == 1 else rank, split, band_rows, dev, render_bands, unshuffle,
                        inflight=inflight, streams=streams, batch=batch)
 
-    # Animated workloads (C5): every frame advances time by 1/60 s through the reference's
-    # Timing::update (frm_timing_update), as the reference's frame loop does
-    # (initialized_app.rs:43-48); frame k of the run renders at time + k/60.
-    clock = frm.Timing()
-    frames_issued = [0]
+    # Animated workloads (C5, HEADLINE_FLY): timed frame k renders frame k of the sequence
+    # (one frame per launch: the scene uniforms change every frame)
     before_frame = None
     if w.animated:
         def before_frame(k):
-            if frames_issued[0] > 0:
-                clock.update(params, 1.0 / 60.0)
-                r.update_parameters_buffer(params)
-            frames_issued[0] += 1
+            r.update_parameters_buffer(frame0 if k == 0 else next(seq))
 
-    tf.run(args.warmup, before_frame)
+    tf.run(args.warmup)
     torch.cuda.synchronize()
     counters.zero_()
     if world > 1:
@@ -359,8 +413,10 @@ def main():
     begin.record(main_stream)
     for s in streams:
         s.wait_event(begin)
+    # rank 0 keeps timed frame 0 (for the golden-frame check) with one device copy on its stream
+    first = torch.empty(w.width * w.height * 4, dtype=torch.uint8, device=dev) if rank == 0 else None
     t0 = time.perf_counter()
-    tf.run(args.steps, before_frame)
+    tf.run(args.steps, before_frame, capture=first)
     for s in streams:
         e = torch.cuda.Event()
         e.record(s)
@@ -373,6 +429,11 @@ def main():
     elapsed = t1 - t0
     span_ms = begin.elapsed_time(end)
     launch_ms = sum(a.elapsed_time(b) for a, b in kev) / max(1, len(kev))
+
+    # the drop-in binding's one-frame-per-frm_render loop on the same workload (rank 0, N = 1)
+    dropin = None
+    if world == 1 and not args.no_dropin:
+        dropin = dropin_loop(frm, torch, w, args, flags, local, camera)
 
     stats_vec = torch.tensor([elapsed, span_ms], dtype=torch.float64, device=dev)
     cnt = counters.clone()
@@ -392,9 +453,11 @@ def main():
         # per-frame device time of the pipelined render (the HIP-event span of the timed
         # region / frames): with F frames in flight launches overlap, so a single launch's
         # start-to-end time (avg_launch_ms) also holds the previous frame's tail
-        avg_kernel_s = span_ms / 1e3 / args.steps
-        wom_per_launch = st["wom_ops"] / args.steps / world
-        achieved = wom_per_launch / avg_kernel_s / 1e12
+        frame_s = span_ms / 1e3 / args.steps
+        # WOM ops of one frame (the whole frame: all ranks' shares of a split frame; AFR: per
+        # rank's frame) and the device time per frame
+        wom_per_frame = st["wom_ops"] / args.steps / (world if split == 1 else 1)
+        achieved = st["wom_ops"] / args.steps / world / frame_s / 1e12  # per GPU
         pmc = pmc_summary(args.workload, world) or {}
         out = {
             "metric": METRIC,
@@ -408,13 +471,16 @@ def main():
             "scaling": "strong" if split > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: deterministic Parameters (fixed camera pose, fixed time), no input data",
+            "data": ("synthetic: deterministic Parameters (" + (
+                "time += 1/60 s per frame" + (", yaw-locked orbit at 0.5 rad/s" if w.fly else "") if w.animated
+                else "fixed camera pose, fixed time") + "), no input data"),
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
                 "pose": args.pose, "frames_in_flight": inflight, "frames_per_launch": batch,
                 "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
-                "animated": "time += 1/60 per frame (Timing::update)" if w.animated else False,
+                "animated": ("time += 1/60 per frame (Timing::update)" + (
+                    " + yaw-locked orbit 0.5 rad/s (Camera::update)" if w.fly else "")) if w.animated else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + "
                                 f"{'RCCL' if backend == 'nccl' else backend + ' (host-staged)'} gather" if split > 1 else
                                 f"alternate-frame rendering x{world}: rank r renders the {args.pose} view "
@@ -440,11 +506,14 @@ def main():
                 "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                 "hbm_write_gbps": pmc.get("hbm_write_gbps"),
                 "hbm_write_frac": pmc.get("hbm_write_frac"),
-                "kernel": "frm::render",
-                "avg_kernel_ms": avg_kernel_s * 1e3,
+                "traffic_split": pmc.get("traffic_split"),
+                "traffic_unit": "HBM bytes per frame (PMC FETCH_SIZE + WRITE_SIZE, march_persistent + shade_pass)",
+                "kernel": "frm::march_persistent + sort + shade_pass (one frame's launches)",
+                "device_ms_per_frame": frame_s * 1e3,
                 "avg_launch_ms": launch_ms,
+                "frames_per_launch": batch,
                 "timing": "HIP events on the render streams: span of the timed region / frames",
-                "algorithmic_ops_per_launch": wom_per_launch,
+                "algorithmic_ops_per_frame": wom_per_frame,
                 "model": "WOM VALU lane-ops counted from fragment.wgsl (DESIGN.md §Roofline)",
             },
             "counters": st,
@@ -453,7 +522,9 @@ def main():
             out["comm"] = {"backend": backend, "ranks": comm_ranks,
                            "data_path": "dist.gather of row bands to rank 0" if split > 1 else "none (timing only)"}
             out["rccl_ranks"] = comm_ranks if backend == "nccl" else None
-        out.update(frame_check(tf.output(), args.workload, args.pose, w.animated))
+        out.update(frame_check(first, args.workload, args.pose))
+        if dropin:
+            out.update(dropin)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(params, w, args.cpu_seconds)
         print(json.dumps(out))

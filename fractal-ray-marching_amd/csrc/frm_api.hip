@@ -53,6 +53,10 @@ struct Slot {
   bool sched_history = false;
   uint32_t sched_w = 0, sched_h = 0;  // frame size of the recorded keys when they cover a whole frame
   bool sched_whole = false;
+  // another slot's launch copied this slot's keys as its scheduling history (on keys_reader):
+  // this slot's next launch, which rewrites them, waits for that copy
+  hipEvent_t keys_read = nullptr;
+  hipStream_t keys_reader = nullptr;
 };
 
 struct frm_ctx {
@@ -124,6 +128,24 @@ uint32_t band_valid_rows(uint32_t height, const BandGeometry& g) {
   return end > height ? g.local_rows - (end - height) : g.local_rows;
 }
 
+// The fractal loop work a frame's parameters ask for (include/frm.h FRM_MAX_NUM_ITERATIONS):
+// trips of the DE's loop per evaluation, after the reference's own loop semantics
+// (Sierpinski's i32 loop runs none for N >= 2^31: compute_scene_uniforms sets n = 0).
+int check_parameters(frm_ctx* ctx, const SceneUniforms& su, const frm_parameters& p) {
+  if (su.family == kMandelbulb && su.n == 0xFFFFFFFFu)
+    return fail(ctx, FRM_ERR_UNSUPPORTED,
+                "num_iterations 0xffffffff: the Mandelbulb's `i <= num_iterations` loop (fragment.wgsl:245) "
+                "never ends; parameters not changed");
+  const uint32_t trips = su.family == kSphere ? 0u : su.n;
+  if (trips > FRM_MAX_NUM_ITERATIONS && !(ctx->flags & FRM_FLAG_UNBOUNDED_ITERATIONS))
+    return fail(ctx, FRM_ERR_UNSUPPORTED,
+                "num_iterations %u (scene %u) above FRM_MAX_NUM_ITERATIONS = %u: every DE runs that many "
+                "loop bodies; create the context with FRM_FLAG_UNBOUNDED_ITERATIONS to allow it; "
+                "parameters not changed",
+                p.num_iterations, p.scene_index, FRM_MAX_NUM_ITERATIONS);
+  return FRM_OK;
+}
+
 int ensure_ready(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
   if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
@@ -193,6 +215,10 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   const uint32_t si = ctx->next_slot;
   Slot& sl = ctx->slots[si];
   if (sl.pending && sl.last_stream != s) FRM_HIP(ctx, hipStreamWaitEvent(s, sl.done, 0));
+  if (sl.keys_reader) {  // another slot's launch read this slot's keys: they are rewritten below
+    if (sl.keys_reader != s) FRM_HIP(ctx, hipStreamWaitEvent(s, sl.keys_read, 0));
+    sl.keys_reader = nullptr;
+  }
   const KernelKind kind = kernel_for(ctx, a.npix);
   a.queue = sl.queue;
   if (kind == kKernelPersistent) {
@@ -259,6 +285,8 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       Slot& dn = ctx->slots[donor];
       if (dn.pending && dn.last_stream != s) FRM_HIP(ctx, hipStreamWaitEvent(s, dn.done, 0));
       FRM_HIP(ctx, hipMemcpyAsync(sl.sched_keys, dn.sched_keys, npix, hipMemcpyDeviceToDevice, s));
+      FRM_HIP(ctx, hipEventRecord(dn.keys_read, s));  // the donor's next launch waits for this copy
+      dn.keys_reader = s;
     }
     const bool history = same || rescale || donor >= 0;
     FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
@@ -317,7 +345,8 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.max_steps %u above %u", config->max_steps,
                 FRM_MAX_STEPS_LIMIT);
   const uint32_t kernels = FRM_FLAG_SIMPLE_KERNEL | FRM_FLAG_PERSISTENT_KERNEL;
-  if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE)) || (config->flags & kernels) == kernels)
+  if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE | FRM_FLAG_UNBOUNDED_ITERATIONS)) ||
+      (config->flags & kernels) == kernels)
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.flags 0x%x: unknown flag or both kernel flags",
                 config->flags);
   int n = 0;
@@ -350,6 +379,8 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
     for (uint32_t i = 0; i < ctx->nslots && rc == FRM_OK; ++i) {
       Slot& sl = ctx->slots[i];
       if ((e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming)) != hipSuccess) rc = hip_fail(ctx, e, "hipEventCreate");
+      else if ((e = hipEventCreateWithFlags(&sl.keys_read, hipEventDisableTiming)) != hipSuccess)
+        rc = hip_fail(ctx, e, "hipEventCreate");
       else if ((e = hipMalloc(&sl.queue, 128)) != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc(queue)");
     }
   } while (0);
@@ -377,6 +408,7 @@ int frm_destroy(frm_ctx* ctx) {
                     (void*)sl.sched_keys, sl.sched_temp})
       if (b) (void)hipFree(b);
     if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.keys_read) (void)hipEventDestroy(sl.keys_read);
     if (i > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
   }
   if (ctx->present_buf) (void)hipFree(ctx->present_buf);
@@ -413,8 +445,12 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
 
 int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters) {
   if (!ctx || !parameters) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/parameters is NULL");
+  SceneUniforms su;
+  compute_scene_uniforms(*parameters, ctx->flags, &su);
+  int rc = check_parameters(ctx, su, *parameters);
+  if (rc) return rc;
   ctx->params = *parameters;
-  compute_scene_uniforms(ctx->params, ctx->flags, &ctx->scene);
+  ctx->scene = su;
   ctx->has_params = true;
   return FRM_OK;
 }
@@ -545,7 +581,8 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
 }
 
 int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* params, uint8_t* dev_dst,
-                           size_t frame_stride_bytes, uint32_t band_rows, uint32_t first_band, uint32_t band_stride,
+                           size_t dst_bytes, size_t frame_stride_bytes, uint32_t band_rows, uint32_t first_band,
+                           uint32_t band_stride,
                            void* stream, uint64_t* dev_counters) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
   if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
@@ -554,9 +591,13 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
                 FRM_MAX_BATCH);
   const uint32_t rows = band_local_rows(ctx->height, band_rows, first_band, band_stride);
   const size_t need = (size_t)rows * ctx->width * 4u;
-  if (frame_stride_bytes < need || frame_stride_bytes % 4u)
-    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "frame stride %zu: below a frame's %zu bytes or not a multiple of 4",
+  if (frame_stride_bytes < need || frame_stride_bytes % 4u || frame_stride_bytes / 4u > 0xFFFFFFFFull)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT,
+                "frame stride %zu: below a frame's %zu bytes, not a multiple of 4 or not below 16 GiB",
                 frame_stride_bytes, need);
+  if (dst_bytes < need || (dst_bytes - need) / frame_stride_bytes < count - 1u)
+    return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, %u frames %zu bytes apart need %zu", dst_bytes,
+                count, frame_stride_bytes, (size_t)(count - 1u) * frame_stride_bytes + need);
   // fetch positions are u32 and every wave's last queue claims run up to two chunks past the
   // end (kQueueHeadroom covers any persistent grid): keep them from wrapping
   if ((uint64_t)rows * ctx->width * count >= 0xFFFFFFFFull - kQueueHeadroom)
@@ -566,6 +607,7 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
   // time-derived constants) and aspect
   SceneUniforms s0;
   compute_scene_uniforms(params[0], ctx->flags, &s0);
+  if (int rc = check_parameters(ctx, s0, params[0])) return rc;
   for (uint32_t k = 1; k < count; ++k) {
     SceneUniforms sk;
     compute_scene_uniforms(params[k], ctx->flags, &sk);
@@ -654,6 +696,7 @@ int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   int rc = wait_slot(ctx, sl);
   if (rc) return rc;
+  if (sl.keys_reader) FRM_HIP(ctx, hipEventSynchronize(sl.keys_read));
   FRM_HIP(ctx, hipMemcpy(sl.sched_keys, keys, n, hipMemcpyHostToDevice));
   return FRM_OK;
 }

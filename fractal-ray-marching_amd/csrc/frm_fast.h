@@ -98,9 +98,13 @@ __device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) 
 // v ^ (m & 0x80000000) in one v_bitop3_b32 (truth table 0x6c: (src0 & src2) ^ src1); left to
 // itself the compiler sometimes splits it into v_and + v_xor
 __device__ __forceinline__ uint32_t xor_sign_(uint32_t v, uint32_t m) {
+#if defined(__gfx950__)
   uint32_t r;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(r) : "v"(m), "v"(v), "s"(0x80000000u));
   return r;
+#else  // v_bitop3 is gfx950-only (ARCH overrides, frm_reload on another device)
+  return v ^ (m & 0x80000000u);
+#endif
 }
 __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
 #ifdef FRM_FAST_V1

@@ -83,7 +83,8 @@ void set_koch(SceneUniforms* u, uint32_t n, float normal_z) {
   u->koch_n2 = u->koch_n1 * mk(1.0f, -1.0f, 1.0f);
   u->koch_offset = offset;
   float scale = 2.0f;
-  for (uint32_t i = 0; i < n; ++i) scale = scale * 1.5f;
+  // 2 * 1.5^n in f32; once it overflows it stays +inf (the loop need not run to n ~ 2^32)
+  for (uint32_t i = 0; i < n && !isinf(scale); ++i) scale = scale * 1.5f;
   u->koch_scale = scale;
   set_tetrahedron(u, top, left, right, back);
 }

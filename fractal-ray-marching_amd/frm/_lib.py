@@ -26,11 +26,12 @@ FRM_MAX_FRAMES_IN_FLIGHT = 8
 FRM_MAX_BATCH = 32
 FRM_DEFAULT_MAX_STEPS = 5000
 FRM_MAX_STEPS_LIMIT = 4194303
-FRM_MAX_NUM_ITERATIONS = 0xFFFFFFFF
+FRM_MAX_NUM_ITERATIONS = 65536
 FRM_NUM_COUNTERS = 8
 FRM_FLAG_SCENE_SPHERE = 0x1
 FRM_FLAG_SIMPLE_KERNEL = 0x2
 FRM_FLAG_PERSISTENT_KERNEL = 0x4
+FRM_FLAG_UNBOUNDED_ITERATIONS = 0x8
 FRM_KERNEL_PERSISTENT = 0
 FRM_KERNEL_SIMPLE = 1
 FRM_BLIT_SRGB = 0x1
@@ -122,7 +123,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("frm_render_bands_batch", ctypes.c_int,
-     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("frm_unshuffle_bands", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,

@@ -115,12 +115,14 @@ class RowTiledFrame:
         self.last_count = count
         self.frames_done += count
 
-    def run(self, n, before_frame=None):
+    def run(self, n, before_frame=None, capture=None):
         """Render, gather and reassemble n frames (asynchronous on the GPU path: callers
         synchronize the device to wait for the last one). Launches take `batch` frames each,
         the last one the remainder. before_frame(k), if given, runs on the host before frame k
         is issued (e.g. to advance animated parameters); for a launch of several frames, before
-        each of its frames, before the launch."""
+        each of its frames, before the launch. capture (rank 0; a flat uint8 tensor of one
+        frame): the first frame of this run is copied into it, in stream order after its
+        render (and reassembly), before its buffers are reused."""
         pending = None
         done = 0
         for k in range(-(-n // self.batch)):
@@ -132,13 +134,25 @@ class RowTiledFrame:
             work = self._issue(k, count)
             if pending is not None:
                 self._finish(*pending)
+                self._capture(pending[0], capture)
             pending = (k, work, count)
         if pending is not None:
             self._finish(*pending)
+            self._capture(pending[0], capture)
+
+    def _capture(self, k, capture):
+        if capture is None or k != 0 or (self.collective and self.rank != 0):
+            return
+        with self._stream(k):
+            capture.copy_(self._frame(k % self.nbuf, 0))
+
+    def _frame(self, buf, b):
+        """Rank 0: frame b of the launch that used buffer set `buf`, flat RGBA8."""
+        if not self.collective:
+            return self.bufs[buf][b * self.nbytes:(b + 1) * self.nbytes]
+        fb = self.height * self.width * 4
+        return self.frames[buf][b * fb:(b + 1) * fb]
 
     def output(self):
         """Rank 0: the last frame, flat RGBA8 (the band buffer itself when world == 1)."""
-        if not self.collective:
-            return self.bufs[self.last][(self.last_count - 1) * self.nbytes:self.last_count * self.nbytes]
-        fb = self.height * self.width * 4
-        return self.frames[self.last][(self.last_count - 1) * fb:self.last_count * fb]
+        return self._frame(self.last, self.last_count - 1)

@@ -104,15 +104,18 @@ class Renderer:
                                                band_stride, stream or None, dev_counters or None))
 
     def render_bands_batch(self, params_list, dev_ptr, frame_stride, band_rows, first_band, band_stride,
-                           stream=0, dev_counters=0):
+                           stream=0, dev_counters=0, dst_bytes=None):
         """frm_render_bands_batch: len(params_list) frames (same scene, camera may differ) in
-        one launch, frame k at dev_ptr + k * frame_stride."""
+        one launch, frame k at dev_ptr + k * frame_stride; dst_bytes = the size of the buffer at
+        dev_ptr (default: len(params_list) * frame_stride)."""
+        if dst_bytes is None:
+            dst_bytes = len(params_list) * frame_stride
         from ._lib import FrmParameters
         arr = (FrmParameters * len(params_list))()
         for k, p in enumerate(params_list):
             ctypes.memmove(ctypes.addressof(arr[k]), p.to_bytes(), ctypes.sizeof(FrmParameters))
         self._check(self._lib.frm_render_bands_batch(self.ctx, len(params_list), ctypes.addressof(arr), dev_ptr,
-                                                     frame_stride, band_rows, first_band, band_stride,
+                                                     dst_bytes, frame_stride, band_rows, first_band, band_stride,
                                                      stream or None, dev_counters or None))
 
     def unshuffle_bands(self, src_ptr, rank_stride, dst_ptr, dst_bytes, band_rows, ranks, stream=0):

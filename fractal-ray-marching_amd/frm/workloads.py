@@ -2,7 +2,7 @@
 import math
 from dataclasses import dataclass
 
-from .parameters import Camera, Parameters
+from .parameters import Camera, Parameters, Timing
 
 # asin(0.6)/0.2: animate_between(4, 9) == 8.0 exactly in f32 -> Mandelbulb power 8.
 POWER8_TIME = 3.2175055
@@ -28,6 +28,7 @@ class Workload:
     sphere: bool = False
     note: str = ""
     animated: bool = False  # frame k renders at time + k/60
+    fly: bool = False  # frame k also orbits the camera (frame_sequence)
 
 
 WORKLOADS = {
@@ -43,7 +44,42 @@ WORKLOADS = {
                    note="16384x16384 animated Mandelbulb, 20 iters, 1024 steps", animated=True),
     "HEADLINE": Workload("headline-mandelbulb-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
                          note="3840x2160 Mandelbulb power 8, 12 iters, 256 steps"),
+    # the reference's own frame loop on the headline scene: every frame Timing::update advances
+    # the time (so the Mandelbulb power moves, fragment.wgsl:75,80-82) and Camera::update orbits
+    # the camera about +y with the yaw locked inwards (camera.rs:100-147); frame 0 is the
+    # headline frame itself
+    "HEADLINE_FLY": Workload("headline-fly-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
+                             note="3840x2160 Mandelbulb from power 8, 12 iters, 256 steps; time += 1/60 and "
+                             "a 0.5 rad/s yaw-locked orbit per frame", animated=True, fly=True),
 }
+
+FLY_ORBIT_RAD_PER_S = 0.5  # = camera.rs:46's rotation speed; 0.48 degrees of orbit per 60 Hz frame
+FRAME_SECONDS = 1.0 / 60.0
+
+
+def frame_sequence(w, pose="P1", dt=FRAME_SECONDS, camera=None):
+    """Parameters of frames 0, 1, 2, ... of workload `w` as the reference's frame loop
+    produces them (InitializedApp::update, initialized_app.rs:43-48: Timing::update, then
+    Camera::update and Parameters::update_camera). Frame 0 is make_parameters(w, pose). Fixed
+    workloads repeat frame 0; animated ones advance time by dt per frame (timing.rs:23-30); fly
+    workloads also orbit the camera at FLY_ORBIT_RAD_PER_S about +y with the yaw locked
+    inwards (camera.rs:119-147). camera = (position, yaw, pitch) replaces the pose's camera.
+    Yields a fresh Parameters object per frame."""
+    p = make_parameters(w, pose=pose)
+    pos, yaw, pitch = POSES[pose] if camera is None else camera
+    cam = Camera(pos, yaw, pitch)
+    p.update_camera(cam)
+    if w.fly:
+        cam.raw.orbit_angle_per_second = FLY_ORBIT_RAD_PER_S
+        cam.raw.lock_yaw_mode = 1  # LockYawMode::Inwards
+    clock = Timing()
+    while True:
+        yield Parameters.from_bytes(p.to_bytes())
+        if w.animated:
+            clock.update(p, dt)
+        if w.fly:
+            cam.update(0, dt)
+            p.update_camera(cam)
 
 
 def make_parameters(w, pose="P1", time=None, width=None, height=None):

@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define FRM_ABI_VERSION 2u  /* 2: frm_config.frames_in_flight (was reserved) */
+#define FRM_ABI_VERSION 3u  /* 2: frm_config.frames_in_flight (was reserved); 3: frm_render_bands_batch
+                               takes dst_bytes, frm_set_parameters bounds the fractal loop work */
 
 /* ---- status codes -------------------------------------------------------- */
 enum {
@@ -79,8 +80,15 @@ _Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
 
 #define FRM_NUM_SCENES 19u            /* parameters.rs:35 (NUM_SCENES)                 */
 #define FRM_DEFAULT_MAX_STEPS 5000u   /* fragment.wgsl:4 (MAX_ITERATIONS)              */
-#define FRM_MAX_NUM_ITERATIONS 0xffffffffu /* any u32, as parameters.rs:31-33 saturates;
-                                          a frame's fractal loops are O(num_iterations) */
+/* Largest fractal loop trip count (Menger/Koch/Sierpinski folds, Mandelbulb bodies - 1) that
+ * frm_set_parameters accepts without FRM_FLAG_UNBOUNDED_ITERATIONS. num_iterations is any u32
+ * in the reference (update_num_iterations saturates, parameters.rs:31-33), and every DE runs
+ * O(num_iterations) loop bodies (fragment.wgsl:181,207,226,245), so a frame near 2^32 runs for
+ * days; such parameters get FRM_ERR_UNSUPPORTED unless the context opted out. Sierpinski's
+ * i32 loop runs no fold for N >= 2^31 (fragment.wgsl:181), which is cheap and always accepted.
+ * The Mandelbulb's `i <= N` loop (fragment.wgsl:245) never ends for N = 0xffffffff (the u32
+ * counter wraps first; the reference hangs too): refused even with the opt-out. */
+#define FRM_MAX_NUM_ITERATIONS 65536u
 #define FRM_MAX_DIMENSION 32768u      /* width/height limit per frame                  */
 
 /* config flags */
@@ -93,6 +101,8 @@ _Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
                                        kernel flag the context picks per launch: simple
                                        below one resident persistent grid of pixels
                                        (frm_kernel_for_pixels), persistent above. */
+#define FRM_FLAG_UNBOUNDED_ITERATIONS 0x8u /* accept num_iterations above FRM_MAX_NUM_ITERATIONS
+                                       (the caller accepts frames whose cost grows with it) */
 
 /* kernels (frm_kernel_for_pixels) */
 #define FRM_KERNEL_PERSISTENT 0u
@@ -150,7 +160,9 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height);
 
 /* ---- uniform upload (replaces Graphics::update_parameters_buffer,
  *      graphics.rs:59-61 → queue.write_buffer, persistent_graphics.rs:167-173).
- *      The struct is copied; it reaches the kernel by value. */
+ *      The struct is copied; it reaches the kernel by value. FRM_ERR_UNSUPPORTED (the previous
+ *      parameters stay) when the scene's fractal loop would exceed FRM_MAX_NUM_ITERATIONS trips
+ *      on a context without FRM_FLAG_UNBOUNDED_ITERATIONS, or never end (see above). */
 int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters);
 
 /* ---- draw (replaces Graphics::render, graphics.rs:91-110). One full frame into
@@ -217,10 +229,12 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
  * per batch. The frames may differ in camera only: params[k] must give the same scene,
  * num_iterations, time-derived scene constants and aspect as params[0]
  * (FRM_ERR_INVALID_ARGUMENT otherwise). The context's parameters become params[count-1].
- * Counters are added over all frames. Bytes per frame are those of frm_render_bands. */
+ * Counters are added over all frames. Bytes per frame are those of frm_render_bands; dev_dst
+ * holds dst_bytes bytes, at least (count - 1) * frame_stride_bytes + one frame's bands
+ * (FRM_ERR_BUFFER_TOO_SMALL otherwise); frame_stride_bytes is a multiple of 4 below 16 GiB. */
 #define FRM_MAX_BATCH 32u
 int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* params,
-                           uint8_t* dev_dst, size_t frame_stride_bytes, uint32_t band_rows,
+                           uint8_t* dev_dst, size_t dst_bytes, size_t frame_stride_bytes, uint32_t band_rows,
                            uint32_t first_band, uint32_t band_stride, void* stream,
                            uint64_t* dev_counters);
 /* Reassemble a frame from per-rank band buffers laid out rank-major in dev_src

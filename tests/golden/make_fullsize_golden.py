@@ -7,8 +7,10 @@ tests/golden/fullsize.json together with the exact 96-byte Parameters of the fra
 GPU tests (tests/test_gpu_fullsize.py) and bench.py's frame check compare whole frames
 without re-running the oracle on the box. Cases: the headline, C2 and C3 at pose P1, C4 at
 P1 and C5 at P1 at its first two animation times (time and time + 1/60, as bench.py's
-Timing::update advances it). The file is rewritten after each case, so an interrupted run
-keeps what it finished."""
+Timing::update advances it); the headline, C2, C3 and C4 at poses P0 and P2; frames 1 and 2 of
+the headline fly-through (HEADLINE_FLY: time += 1/60 and a yaw-locked orbit per frame,
+frm.frame_sequence; its frame 0 is HEADLINE_P1). The file is rewritten after each case, so an
+interrupted run keeps what it finished."""
 import hashlib
 import json
 import os
@@ -28,22 +30,29 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fullsize.json")
 
 
 def cases():
-    """(key, workload name, Parameters) in the order they are rendered."""
+    """(key, workload name, pose, Parameters) in the order they are rendered."""
     for name in ("HEADLINE", "C2", "C3", "C4"):
         w = frm.WORKLOADS[name]
-        yield f"{name}_P1", name, frm.make_parameters(w, pose="P1")
+        yield f"{name}_P1", name, "P1", frm.make_parameters(w, pose="P1")
     w = frm.WORKLOADS["C5"]
     p = frm.make_parameters(w, pose="P1")
-    yield "C5_P1_t0", "C5", p
+    yield "C5_P1_t0", "C5", "P1", p
     p1 = frm.make_parameters(w, pose="P1")
     frm.Timing().update(p1, 1.0 / 60.0)  # the second frame bench.py renders
-    yield "C5_P1_t1", "C5", p1
+    yield "C5_P1_t1", "C5", "P1", p1
+    for name in ("HEADLINE", "C2", "C3", "C4"):
+        for pose in ("P0", "P2"):
+            yield f"{name}_{pose}", name, pose, frm.make_parameters(frm.WORKLOADS[name], pose=pose)
+    seq = frm.frame_sequence(frm.WORKLOADS["HEADLINE_FLY"], pose="P1")
+    next(seq)  # frame 0 = HEADLINE_P1
+    for k in (1, 2):
+        yield f"HEADLINE_FLY_P1_f{k}", "HEADLINE_FLY", "P1", next(seq)
 
 
 def main(only):
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
     threads = os.cpu_count() or 1
-    for key, name, p in cases():
+    for key, name, pose, p in cases():
         if (only and key not in only and name not in only) or key in out:
             continue
         w = frm.WORKLOADS[name]
@@ -52,7 +61,7 @@ def main(only):
         r = fo.render(p, w.width, w.height, w.max_steps, flags=flags, threads=threads)
         out[key] = {
             "workload": name, "width": w.width, "height": w.height, "max_steps": w.max_steps,
-            "flags": flags, "pose": "P1", "time": float(np.float32(p.time)),
+            "flags": flags, "pose": pose, "time": float(np.float32(p.time)),
             "params": p.to_bytes().hex(),
             "sha256": hashlib.sha256(r["rgba"].tobytes()).hexdigest(),
             "counters": [int(c) for c in r["counters"]],

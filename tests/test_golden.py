@@ -54,3 +54,27 @@ def test_oracle_de_matches_golden(oracle):
             d, col, _ = oracle.scene_de(p, pts)
             assert np.array_equal(d.view(np.uint32), g[f"s{scene}_n{n}_d"].view(np.uint32))
             assert np.array_equal(col, g[f"s{scene}_n{n}_c"])
+
+
+def test_default_parameters_blob_and_oracle_at_5000_steps(oracle):
+    """tests/golden/defaults.json (make_defaults_golden.py): the DEFAULT frame's Parameters are
+    Parameters::default() + update_aspect(1920, 1080) + update_camera(Camera::default())
+    (initialized_app.rs:24, camera.rs:176-187), every sweep blob is P1 with the recorded scene,
+    iterations and time, and the oracle still renders the cheap frames' recorded hashes and
+    counters at 5000 steps (the GPU side is tests/test_gpu_defaults.py)."""
+    g = json.load(open(os.path.join(GOLD, "defaults.json")))
+    p = frm.Parameters()
+    p.update_aspect(1920, 1080)
+    p.update_camera(frm.Camera())
+    assert p.to_bytes().hex() == g["DEFAULT"]["params"]
+    for key, e in g.items():
+        if key.startswith("S"):
+            q = frm.make_parameters(frm.WORKLOADS["C2"], pose="P1")
+            q.scene_index, q.num_iterations, q.time = e["scene_index"], e["num_iterations"], e["time"]
+            assert q.to_bytes().hex() == e["params"], key
+    for key in ("DEFAULT", "S0_N3_t0", "S16_N3_t0"):
+        e = g[key]
+        r = oracle.render(frm.Parameters.from_bytes(bytes.fromhex(e["params"])), e["width"], e["height"],
+                          e["max_steps"], threads=os.cpu_count())
+        assert hashlib.sha256(r["rgba"].tobytes()).hexdigest() == e["sha256"], key
+        assert [int(c) for c in r["counters"]] == e["counters"], key

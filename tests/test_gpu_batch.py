@@ -88,6 +88,15 @@ def test_batch_rejects_frames_that_differ_beyond_the_camera(frm_lib):
             assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
         with pytest.raises(frm.FrmError):
             r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), w * h * 4, h, 0, 1)
+        # the destination must hold every frame: (count - 1) strides + one frame
+        for n, stride in ((2, w * h * 4 + 4), (3, w * h * 4)):
+            with pytest.raises(frm.FrmError) as e:
+                r.render_bands_batch([a] * n, buf.data_ptr(), stride, h, 0, 1, dst_bytes=buf.numel())
+            assert e.value.code == _lib.FRM_ERR_BUFFER_TOO_SMALL
+        with pytest.raises(frm.FrmError) as e:  # strides of 16 GiB and more do not fit the kernel's word stride
+            r.render_bands_batch([a] * 2, buf.data_ptr(), 1 << 34, h, 0, 1, dst_bytes=1 << 35)
+        assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
+        r.render_bands_batch([a] * 2, buf.data_ptr(), w * h * 4, h, 0, 1, dst_bytes=buf.numel())
 
 
 def test_batch_of_max_frames_two_slots(frm_lib, oracle):

@@ -42,6 +42,40 @@ def test_num_iterations_above_old_cap(frm_lib, oracle, scene, iters):
     assert np.array_equal(img, ref["rgba"])
 
 
+def test_unbounded_num_iterations_are_refused_not_rendered(frm_lib, oracle):
+    """Parameters whose fractal loop never ends (Mandelbulb N = 0xffffffff: `i <= N` wraps,
+    fragment.wgsl:245) are refused even with FRM_FLAG_UNBOUNDED_ITERATIONS; loops above
+    FRM_MAX_NUM_ITERATIONS trips are refused unless the context opted out. A refused update keeps
+    the previous parameters (the next frame renders them); the opt-out renders the reference's
+    semantics bit-exact."""
+    from frm import _lib
+
+    w, h = 16, 9
+    good = params_for(18, 12, frm.POWER8_TIME, w, h)
+    with frm.Renderer(device=0, max_steps=64) as r:
+        r.resize(w, h)
+        r.update_parameters_buffer(good)
+        for scene, iters in ((18, 0xFFFFFFFF), (18, frm.FRM_MAX_NUM_ITERATIONS + 1), (0, 0xFFFFFFFE),
+                             (16, frm.FRM_MAX_NUM_ITERATIONS + 1), (15, 2 ** 31 - 1)):
+            with pytest.raises(frm.FrmError) as e:
+                r.update_parameters_buffer(params_for(scene, iters, frm.POWER8_TIME, w, h))
+            assert e.value.code == _lib.FRM_ERR_UNSUPPORTED
+        r.update_parameters_buffer(params_for(0, frm.FRM_MAX_NUM_ITERATIONS, 0.0, w, h))  # the cap itself
+        r.update_parameters_buffer(good)
+        with pytest.raises(frm.FrmError):
+            r.update_parameters_buffer(params_for(18, 0xFFFFFFFF, frm.POWER8_TIME, w, h))
+        r.render(stats=False)
+        assert np.array_equal(r.read_frame(), oracle.render(good, w, h, 64)["rgba"])
+    with frm.Renderer(device=0, max_steps=8, flags=frm.FRM_FLAG_UNBOUNDED_ITERATIONS) as r:
+        r.resize(w, h)
+        with pytest.raises(frm.FrmError):
+            r.update_parameters_buffer(params_for(18, 0xFFFFFFFF, frm.POWER8_TIME, w, h))
+        p = params_for(0, frm.FRM_MAX_NUM_ITERATIONS + 7, 0.0, w, h)
+        r.update_parameters_buffer(p)
+        r.render(stats=False)
+        assert np.array_equal(r.read_frame(), oracle.render(p, w, h, 8)["rgba"])
+
+
 def test_pixel_keys_roundtrip_and_injected_orders_keep_bytes(frm_lib, oracle):
     """The scheduling diagnostics (frm_debug_pixel_keys / frm_debug_set_pixel_keys): the keys the
     persistent kernel records are 16 log2(bodies + 1) per pixel (0 only where a pixel ran no
