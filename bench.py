@@ -204,7 +204,7 @@ def dropin_loop(frm, torch, w, args, flags, local, camera):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(n):
-            if k > 0 and w.animated:
+            if k > 0 and w.moving:
                 r.update_parameters_buffer(next(seq))
             st = r.render(stats=True)
             steps += st["march_steps"]
@@ -242,12 +242,19 @@ def launch_ranks(args):
 GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
 
+def motion(w):
+    """What changes from frame to frame (frm.frame_sequence)."""
+    parts = (["time += 1/60 s per frame (Timing::update)"] if w.animated else []) + (
+        ["yaw-locked orbit at 0.5 rad/s (Camera::update)"] if w.fly else [])
+    return " + ".join(parts) if parts else "fixed camera pose, fixed time"
+
+
 def golden_key(workload, pose):
     """The golden frame that equals frame 0 of the timed sequence (frm.frame_sequence): the
     fixed frame itself; C5's first animation time; the fly-through's frame 0 is the headline."""
     if workload == "C5":
         return f"C5_{pose}_t0"
-    if workload == "HEADLINE_FLY":
+    if workload.startswith("HEADLINE_"):  # HEADLINE_FLY / _TIME / _ORBIT: frame 0 is the headline
         return f"HEADLINE_{pose}"
     return f"{workload}_{pose}"
 
@@ -337,7 +344,7 @@ def main():
     # 1.385-1.402, profiles/round2/batch32/). Auto: the timed frames in equal launches of at
     # most 16 (20 frames: 2 x 10). Animated workloads change the scene every frame: one frame
     # per launch.
-    if w.animated:
+    if w.moving:
         batch = 1
     elif args.batch:
         batch = max(1, min(args.batch, frm.FRM_MAX_BATCH))
@@ -396,7 +403,7 @@ def main():
     # Animated workloads (C5, HEADLINE_FLY): timed frame k renders frame k of the sequence
     # (one frame per launch: the scene uniforms change every frame)
     before_frame = None
-    if w.animated:
+    if w.moving:
         def before_frame(k):
             r.update_parameters_buffer(frame0 if k == 0 else next(seq))
 
@@ -471,16 +478,13 @@ def main():
             "scaling": "strong" if split > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("synthetic: deterministic Parameters (" + (
-                "time += 1/60 s per frame" + (", yaw-locked orbit at 0.5 rad/s" if w.fly else "") if w.animated
-                else "fixed camera pose, fixed time") + "), no input data"),
+            "data": "synthetic: deterministic Parameters (" + motion(w) + "), no input data",
             "config": {
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
                 "pose": args.pose, "frames_in_flight": inflight, "frames_per_launch": batch,
                 "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
-                "animated": ("time += 1/60 per frame (Timing::update)" + (
-                    " + yaw-locked orbit 0.5 rad/s (Camera::update)" if w.fly else "")) if w.animated else False,
+                "animated": motion(w) if w.moving else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + "
                                 f"{'RCCL' if backend == 'nccl' else backend + ' (host-staged)'} gather" if split > 1 else
                                 f"alternate-frame rendering x{world}: rank r renders the {args.pose} view "

@@ -21,6 +21,10 @@ using namespace frm;
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
 static constexpr uint32_t kDefaultServiceMin = 24;  // swept 16..36 on MI355X (round 1: 20); round-2 kernel: headline 16/20/24/28 = 11.43/11.36/11.18/11.24 ms, C2 flat
+// Persistent kernel: a wave whose lane has spent this many cost units (Mandelbulb bodies, DEs
+// for the other families) on its current pixel runs at raised issue priority (s_setprio) until it
+// holds no such pixel. FRM_PRIO_COST overrides it (0 = off).
+static constexpr uint32_t kDefaultPrioCost = 0;
 // Kernel choice without a FRM_FLAG_*_KERNEL flag: below one resident persistent grid
 // (6 blocks of 256 lanes per CU for the Mandelbulb) a launch has fewer pixels than lanes,
 // and the persistent kernel's fixed costs (pixel sort, grid, separate shading pass) outweigh
@@ -57,6 +61,11 @@ struct Slot {
   // this slot's next launch, which rewrites them, waits for that copy
   hipEvent_t keys_read = nullptr;
   hipStream_t keys_reader = nullptr;
+  // the launch the keys come from: its last frame's camera and records (reprojection when the
+  // next launch's camera differs, frm_sched.hip reproject_keys)
+  FrameUniforms sched_f{};
+  size_t sched_rec_base = 0;
+  bool sched_records = false;
 };
 
 struct frm_ctx {
@@ -76,6 +85,8 @@ struct frm_ctx {
   size_t present_cap = 0;
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   uint32_t service_min = kDefaultServiceMin;
+  uint32_t prio_cost = kDefaultPrioCost;
+  bool reproject = true;  // FRM_NO_REPROJECT=1 turns the key reprojection off (A/B experiments)
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
@@ -132,7 +143,7 @@ uint32_t band_valid_rows(uint32_t height, const BandGeometry& g) {
 // trips of the DE's loop per evaluation, after the reference's own loop semantics
 // (Sierpinski's i32 loop runs none for N >= 2^31: compute_scene_uniforms sets n = 0).
 int check_parameters(frm_ctx* ctx, const SceneUniforms& su, const frm_parameters& p) {
-  if (su.family == kMandelbulb && su.n == 0xFFFFFFFFu)
+  if (is_mandelbulb(su.family) && su.n == 0xFFFFFFFFu)
     return fail(ctx, FRM_ERR_UNSUPPORTED,
                 "num_iterations 0xffffffff: the Mandelbulb's `i <= num_iterations` loop (fragment.wgsl:245) "
                 "never ends; parameters not changed");
@@ -167,6 +178,7 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.counters = counters;
   a.npix = band_valid_rows(ctx->height, a.g) * ctx->width;
   a.service_min = ctx->service_min;
+  a.prio_cost = ctx->prio_cost;
   a.batch = 1;
   a.rec_stride = local_rows * ctx->width;
   a.out_stride = local_rows * ctx->width;
@@ -224,6 +236,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   if (kind == kKernelPersistent) {
     const size_t need = (size_t)a.g.local_rows * a.f.width * a.batch;
     if (need > sl.records_cap) {  // grows outside the steady state (first frame of a size)
+      sl.sched_records = false;  // the records the keys came from are gone
       int rc = wait_slot(ctx, sl);
       if (rc) return rc;
       if (sl.records) FRM_HIP(ctx, hipFree(sl.records));
@@ -289,6 +302,24 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       dn.keys_reader = s;
     }
     const bool history = same || rescale || donor >= 0;
+    // the keys' frame was seen from another camera: project them into this launch's
+    FrameUniforms nf = a.f;
+    if (a.batch > 1) {
+      memcpy(nf.row, a.cams[0].row, sizeof(nf.row));
+      nf.origin = a.cams[0].origin;
+    }
+    if (same && sl.sched_records && ctx->reproject &&
+        (memcmp(nf.row, sl.sched_f.row, sizeof(nf.row)) != 0 || memcmp(&nf.origin, &sl.sched_f.origin, sizeof(v3)) != 0)) {
+      ReprojectArgs ra;
+      ra.prev = sl.sched_f;
+      ra.next = nf;
+      ra.g = a.g;
+      ra.tails = a.tails + sl.sched_rec_base;
+      ra.geom = a.geom + sl.sched_rec_base;
+      ra.npix = npix;
+      ra.valid_rows = npix / a.f.width;
+      FRM_HIP(ctx, reproject_keys(ra, sl.sched_keys, sl.sched_order, s));
+    }
     FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
                                  sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
     a.pixel_order = sl.sched_order;
@@ -298,6 +329,9 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
     sl.sched_whole = whole;
     sl.sched_w = a.f.width;
     sl.sched_h = a.f.height;
+    sl.sched_f = a.f;  // the keys shade_pass records are the last frame's (a.f = its camera)
+    sl.sched_rec_base = (size_t)(a.batch - 1u) * a.rec_stride;
+    sl.sched_records = true;
     a.debug = (unsigned long long*)(sl.queue + 8);  // bytes 32..71 of the queue block
     FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, sizeof(unsigned int), s));
 #ifdef FRM_STAMPS
@@ -345,7 +379,7 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.max_steps %u above %u", config->max_steps,
                 FRM_MAX_STEPS_LIMIT);
   const uint32_t kernels = FRM_FLAG_SIMPLE_KERNEL | FRM_FLAG_PERSISTENT_KERNEL;
-  if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE | FRM_FLAG_UNBOUNDED_ITERATIONS)) ||
+  if ((config->flags & ~(kernels | FRM_FLAG_SCENE_SPHERE | FRM_FLAG_UNBOUNDED_ITERATIONS | FRM_FLAG_HW_MATH)) ||
       (config->flags & kernels) == kernels)
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.flags 0x%x: unknown flag or both kernel flags",
                 config->flags);

@@ -124,7 +124,7 @@ void compute_scene_uniforms(const frm_parameters& p, uint32_t flags, SceneUnifor
     case 16: set_koch(u, p.num_iterations, (float)sqrt(3.0)); break;
     case 17: set_koch(u, p.num_iterations, animate_between(t, (float)sqrt(3.0), 4.0f)); break;
     case 18:
-      u->family = kMandelbulb;
+      u->family = (flags & FRM_FLAG_HW_MATH) ? kMandelbulbHw : kMandelbulb;
       u->mb_power = animate_between(t, 4.0f, 9.0f);
       u->mb_power_m1 = u->mb_power - 1.0f;
       u->mb_bailout = 100.0f;
@@ -165,7 +165,8 @@ uint64_t wom_ops(const SceneUniforms& u, const uint64_t* c) {
     case kMenger: de_ops = de_calls * (14 + 21 * n); break;
     case kSierpinski: de_ops = de_calls * (28 + 30 * n); break;
     case kKoch: de_ops = de_calls * (32 + 18 * n); break;
-    case kMandelbulb: de_ops = c[kCntBodies] * 57 + c[kCntBailouts] * 5 + de_calls * 6; break;
+    case kMandelbulb:
+    case kMandelbulbHw: de_ops = c[kCntBodies] * 57 + c[kCntBailouts] * 5 + de_calls * 6; break;
     default: de_ops = de_calls * 5; break;
   }
   // march-step overhead 10 per step; per pixel ray generation 28; per hit the normal

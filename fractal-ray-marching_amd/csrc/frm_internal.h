@@ -47,6 +47,9 @@ struct KernelArgs {
   ShadeTail* tails;               // persistent kernel: local_rows * width march-end records
   uint32_t npix;                  // persistent kernel: pixels of the launch (= fetch positions)
   uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
+  uint32_t prio_cost;             // persistent kernel: a wave holding a pixel that has run this many
+                                  // cost units (Mandelbulb bodies / DEs) issues at raised priority
+                                  // (0: never)
   unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
   const uint32_t* pixel_order;    // persistent kernel: local pixel index at each fetch position
   uint8_t* pixel_key;             // persistent kernel: cost key per local pixel (out)
@@ -61,6 +64,18 @@ struct KernelArgs {
   FrameCamera cams[kMaxBatch];
 };
 
+// Forward projection of the previous launch's cost keys into a moved camera (frm_sched.hip):
+// the records and camera of the launch whose keys the slot holds (its last frame), the camera
+// of the next launch's first frame, and the (unchanged) band geometry.
+struct ReprojectArgs {
+  FrameUniforms prev, next;
+  BandGeometry g;
+  const ShadeTail* tails;  // the previous launch's last frame's records
+  const ShadeGeom* geom;
+  uint32_t npix;           // local pixels (= valid_rows * width)
+  uint32_t valid_rows;
+};
+
 #ifndef FRM_MARCH_BLOCK
 #define FRM_MARCH_BLOCK 256
 #endif
@@ -70,7 +85,7 @@ constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
 #if !defined(__HIPCC_RTC__)  // host-side launchers; hiprtc only needs the types above
 // Render kernels compiled at run time from edited sources (frm_reload.hip), per DE family
 // (Family in frm_scene.h) and ITERS.
-constexpr uint32_t kNumFamilies = 5;
+constexpr uint32_t kNumFamilies = 6;
 struct ReloadedKernels {
   hipModule_t module = nullptr;
   hipFunction_t simple[kNumFamilies][2] = {};
@@ -98,6 +113,9 @@ hipError_t schedule_pixels(uint32_t npix, bool has_history, const uint8_t* key, 
                            const uint32_t* iota, uint32_t* order, void* temp, size_t temp_bytes,
                            hipStream_t stream);
 hipError_t fill_iota(uint32_t* out, uint32_t n, hipStream_t stream);
+// Forward projection of keys (npix local pixels) from a.prev's camera into a.next's; scratch holds
+// npix u32 (the fetch order array, rewritten by the sort afterwards).
+hipError_t reproject_keys(const ReprojectArgs& a, uint8_t* keys, uint32_t* scratch, hipStream_t stream);
 // Whole-frame key map sw x sh -> dw x dh, nearest neighbour (history across a resize).
 hipError_t rescale_keys(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                         hipStream_t stream);

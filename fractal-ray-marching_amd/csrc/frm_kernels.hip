@@ -96,6 +96,7 @@ hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t 
     case kSierpinski: eval_scene_fam<kSierpinski>(s, pts, n, dist, color, stream); break;
     case kKoch: eval_scene_fam<kKoch>(s, pts, n, dist, color, stream); break;
     case kMandelbulb: eval_scene_fam<kMandelbulb>(s, pts, n, dist, color, stream); break;
+    case kMandelbulbHw: eval_scene_fam<kMandelbulbHw>(s, pts, n, dist, color, stream); break;
     default: eval_scene_fam<kSphere>(s, pts, n, dist, color, stream); break;
   }
   return hipGetLastError();
@@ -172,6 +173,7 @@ hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, 
     case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream, rk);
     case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream, rk);
     case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream, rk);
+    case kMandelbulbHw: return launch_family<kMandelbulbHw>(args, kind, cu_count, stream, rk);
     default: return launch_family<kSphere>(args, kind, cu_count, stream, rk);
   }
 }

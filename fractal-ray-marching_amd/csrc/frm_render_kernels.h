@@ -106,6 +106,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 
   const FrameUniforms& f = a.f;
   const SceneUniforms& su = a.s;
+  constexpr bool kMb = is_mandelbulb(FAM);     // resumable body loop
+  constexpr bool kHw = FAM == kMandelbulbHw;   // FRM_FLAG_HW_MATH
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t lane_bit = 1ull << lane;
   constexpr bool multi = MULTI;
@@ -119,6 +121,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   // wave-uniform state: current chunk of 64 fetched pixels, how many were handed out
   uint32_t slots_used = kChunk;
   bool exhausted = false;
+  bool raised = false;  // wave priority raised (a lane holds a long-running pixel)
   uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
 #ifdef FRM_COUNT_EXACT
   uint64_t n_dbg_total = 0, n_dbg_exact = 0;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     // Body phase (Mandelbulb): one loop body per computing lane per iteration, until
     // a.service_min lanes wait for a service pass (finished DE, or idle with work left)
     // or no lane computes. The service pass costs the same however many lanes take part.
-    if constexpr (FAM == kMandelbulb) {
+    if constexpr (kMb) {
       // The loop keeps its lane sets as wave-uniform masks (SGPRs): `pending` predicates the
       // body directly (inverse ballot -> exec) and one ballot per iteration retires lanes,
       // instead of a per-lane flag merged under exec masks every iteration.
@@ -171,12 +174,12 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           n_dbg_total++;
           if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
 #endif
-          mb_step(su, q, mag, z, dr);
+          mb_step<kHw>(su, q, mag, z, dr);
           body++;
           if (body > n_iter) {
             fin = 1;  // N+1 bodies: the distance uses the last loop-top magnitude
           } else {
-            mag = mb_length(z);
+            mag = mb_length<kHw>(z);
             fin = mag > su.mb_bailout;
           }
         }
@@ -198,17 +201,17 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     // split) when every consuming lane's magnitude is positive, normal and finite
     // (wave-uniform test; same bits)
     bool plain_log = true;
-    if constexpr (FAM == kMandelbulb)
+    if constexpr (kMb && !kHw)
       plain_log = ballot(cons && !__builtin_amdgcn_classf(mag, 0x100 /* +normal */)) == 0;
     if (cons) {
       done = false;
-      if constexpr (FAM == kMandelbulb) {
+      if constexpr (kMb) {
         FRM_SUB_BEGIN();
-#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)  // measurement build: one path for every lane
-        (void)plain_log;
-        de = mb_distance_posnormal(mag, dr);
-#elif defined(__HIP_DEVICE_COMPILE__)
-        de = plain_log ? mb_distance_posnormal(mag, dr) : mb_distance(mag, dr);
+#if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (kHw)
+          de = mb_distance_hw(mag, dr);
+        else
+          de = plain_log ? mb_distance_posnormal(mag, dr) : mb_distance(mag, dr);
 #else
         (void)plain_log;
         de = mb_distance(mag, dr);
@@ -344,17 +347,30 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       const float e = kMinDistance;
       const float ex = (kq == 0u || kq == 3u) ? e : -e, ey = (kq >= 2u) ? e : -e, ez = (kq == 1u || kq == 3u) ? e : -e;
       q = mk(is_tap ? r.x + ex : r.x, is_tap ? r.y + ey : r.y, is_tap ? r.z + ez : r.z);
-      if constexpr (FAM == kMandelbulb) {
+      if constexpr (kMb) {
         z = q;
         dr = 1.f;
         body = 0;
-        mag = mb_length(q);
+        mag = mb_length<kHw>(q);
         done = mag > su.mb_bailout;
       } else {
         DeCount unused = {0u, 0u};
         de = scene_de<FAM, ITERS>(su, q, unused);
         done = true;
         pix_cost++;  // fixed-trip families: the scheduling cost unit is one DE
+      }
+    }
+
+    // a pixel whose march has already run long is likely the frame's critical path: its wave
+    // issues first among the SIMD's waves while it holds one (scheduling only, same bytes)
+    if (a.prio_cost) {
+      const bool hot = ballot(pix != kIdle && pix_cost >= a.prio_cost) != 0;
+      if (hot != raised) {
+        if (hot)
+          __builtin_amdgcn_s_setprio(3);
+        else
+          __builtin_amdgcn_s_setprio(0);
+        raised = hot;
       }
     }
 

@@ -44,7 +44,10 @@ enum Family : uint32_t {
   kKoch = 2,        // scenes 16-17         fragment.wgsl:213-238
   kMandelbulb = 3,  // scene 18             fragment.wgsl:240-271
   kSphere = 4,      // build extension (BASELINE config C1), not in the reference
+  kMandelbulbHw = 5,  // scene 18 with FRM_FLAG_HW_MATH: hardware transcendentals (not bit-exact)
 };
+// the Mandelbulb family, in either math (frm builtins / hardware transcendentals)
+constexpr bool is_mandelbulb(uint32_t fam) { return fam == kMandelbulb || fam == kMandelbulbHw; }
 
 // Constants of fragment.wgsl:1-16 and 92-94 (abstract floats rounded once to f32).
 constexpr float kMaxTotalDistance = 1000.0f;          // :2
@@ -217,13 +220,14 @@ FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
   sincos_(phi * P, &sp, &cp);
   z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
 }
-#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
-// MEASUREMENT BUILD ONLY (-DFRM_HW_MATH, tools/gpu_hw_math.sh; never the product): the
-// Mandelbulb body and distance with gfx950's hardware transcendentals, as a Vulkan driver
-// lowers fragment.wgsl's builtins: log2/exp2 -> v_log_f32/v_exp_f32, sin/cos -> v_sin/v_cos
-// (argument in revolutions), sqrt -> v_sqrt_f32, a / b -> a * v_rcp_f32(b); acos and atan2
-// keep their polynomials on those primitives. Not bit-exact with the oracle by design: DESIGN
-// §5 prices exact math against it.
+#if defined(__HIP_DEVICE_COMPILE__)
+// FRM_FLAG_HW_MATH (opt-in, never the default; kMandelbulbHw): the Mandelbulb body, magnitude and
+// distance on gfx950's hardware transcendentals, as a Vulkan driver lowers fragment.wgsl's
+// builtins: log2/exp2 -> v_log_f32/v_exp_f32, sin/cos -> v_sin/v_cos (argument in revolutions),
+// sqrt -> v_sqrt_f32, a / b -> a * v_rcp_f32(b); acos and atan2 keep their polynomials on those
+// primitives. Within WGSL's builtin accuracy bounds but not bit-exact with the oracle: its frames
+// are gated by the classified P1 comparison against precise builtins (tests/test_gpu_hw_math.py,
+// DESIGN.md section 3) instead of P0.
 __device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float hw_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 __device__ __forceinline__ void hw_sincos(float x, float* s, float* c) {
@@ -269,6 +273,9 @@ __device__ __forceinline__ void mb_body_hw(const SceneUniforms& u, v3 c, float r
   hw_sincos(phi * P, &sp, &cp);
   z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
 }
+__device__ __forceinline__ float mb_distance_hw(float r, float dr) {
+  return hw_div((0.5f * (__builtin_amdgcn_logf(r) * 0.6931471805599453f)) * r, dr);
+}
 #endif
 
 // distance = 0.5 * log(magnitude) * magnitude / magnitude_derivative, fragment.wgsl:269
@@ -278,11 +285,7 @@ FRM_HD float mb_distance_posfinite(float r, float dr) { return ((0.5f * log_posf
 #if defined(__HIP_DEVICE_COMPILE__)
 // mb_distance for positive normal finite r (integer exponent split, frm_fast.h): same bits.
 __device__ __forceinline__ float mb_distance_posnormal(float r, float dr) {
-#ifdef FRM_HW_MATH
-  return hw_div((0.5f * (__builtin_amdgcn_logf(r) * 0.6931471805599453f)) * r, dr);
-#else
   return ((0.5f * log_posnormal(r)) * r) / dr;
-#endif
 }
 #endif
 
@@ -352,13 +355,15 @@ __device__ __forceinline__ bool length_small(v3 a) {
 
 
 // One Mandelbulb body; on the GPU the wave takes the tame fast path (frm_fast.h) when all
-// its active lanes have tame operands. Bit-identical to mb_body either way.
+// its active lanes have tame operands. Bit-identical to mb_body either way. HW: the hardware-
+// transcendental body (FRM_FLAG_HW_MATH; host builds have no such math and run mb_body).
+template <bool HW = false>
 FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
-#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
-  mb_body_hw(u, c, r, z, dr);
-  return;
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (HW) {
+    mb_body_hw(u, c, r, z, dr);
+    return;
+  }
   if (ballot(!mb_tame(z, r)) == 0) {
     mb_body_tame(u, c, r, z, dr);
     return;
@@ -367,11 +372,10 @@ FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
   mb_body(u, c, r, z, dr);
 }
 // length(z) for the Mandelbulb magnitude; fast sqrt unless a lane has 0 < |z|^2 < 2^-96.
+template <bool HW = false>
 FRM_HD float mb_length(v3 z) {
-#if defined(FRM_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
-  return hw_sqrt(dot(z, z));
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (HW) return hw_sqrt(dot(z, z));
   if (ballot(length_small(z)) == 0) return length_nosmall(z);
 #endif
   return length(z);
@@ -379,22 +383,25 @@ FRM_HD float mb_length(v3 z) {
 
 // mandelbulb(position, power, bailout), fragment.wgsl:240-271: N+1 bodies; the distance
 // uses the last magnitude computed at the top of the loop.
-template <bool ITERS>
+template <bool ITERS, bool HW = false>
 FRM_HD float de_mandelbulb(const SceneUniforms& u, v3 p, DeCount& cnt) {
   const uint32_t n = iterations<ITERS>(u.n);
   v3 z = p;
   float dr = 1.0f;
   float r = 0.0f;
   for (uint32_t i = 0;; ++i) {
-    r = mb_length(z);
+    r = mb_length<HW>(z);
     if (r > u.mb_bailout) {
       cnt.bailouts++;
       break;
     }
-    mb_step(u, p, r, z, dr);
+    mb_step<HW>(u, p, r, z, dr);
     cnt.bodies++;
     if (i == n) break;
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (HW) return mb_distance_hw(r, dr);
+#endif
   return mb_distance(r, dr);
 }
 
@@ -406,6 +413,7 @@ FRM_HD float scene_de(const SceneUniforms& u, v3 p, DeCount& cnt) {
   else if constexpr (FAM == kSierpinski) return de_sierpinski<ITERS>(u, p);
   else if constexpr (FAM == kKoch) return de_koch<ITERS>(u, p);
   else if constexpr (FAM == kMandelbulb) return de_mandelbulb<ITERS>(u, p, cnt);
+  else if constexpr (FAM == kMandelbulbHw) return de_mandelbulb<ITERS, true>(u, p, cnt);
   else return de_sphere(p);
 }
 

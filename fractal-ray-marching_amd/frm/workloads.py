@@ -28,7 +28,12 @@ class Workload:
     sphere: bool = False
     note: str = ""
     animated: bool = False  # frame k renders at time + k/60
-    fly: bool = False  # frame k also orbits the camera (frame_sequence)
+    fly: bool = False  # frame k orbits the camera (frame_sequence)
+
+    @property
+    def moving(self):
+        """Frames differ (time or camera): one frame per launch, history from another frame."""
+        return self.animated or self.fly
 
 
 WORKLOADS = {
@@ -51,6 +56,11 @@ WORKLOADS = {
     "HEADLINE_FLY": Workload("headline-fly-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
                              note="3840x2160 Mandelbulb from power 8, 12 iters, 256 steps; time += 1/60 and "
                              "a 0.5 rad/s yaw-locked orbit per frame", animated=True, fly=True),
+    # its two halves (scheduling diagnostics, tools/fly_probe.py): the time alone, the orbit alone
+    "HEADLINE_TIME": Workload("headline-time-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
+                              note="HEADLINE_FLY without the orbit (time += 1/60 per frame)", animated=True),
+    "HEADLINE_ORBIT": Workload("headline-orbit-4k", 3840, 2160, 18, 12, 256, POWER8_TIME,
+                               note="HEADLINE_FLY at a fixed time (the orbit alone)", fly=True),
 }
 
 FLY_ORBIT_RAD_PER_S = 0.5  # = camera.rs:46's rotation speed; 0.48 degrees of orbit per 60 Hz frame

@@ -103,6 +103,14 @@ _Static_assert(sizeof(frm_parameters) == 96, "frm_parameters must be 96 bytes");
                                        (frm_kernel_for_pixels), persistent above. */
 #define FRM_FLAG_UNBOUNDED_ITERATIONS 0x8u /* accept num_iterations above FRM_MAX_NUM_ITERATIONS
                                        (the caller accepts frames whose cost grows with it) */
+#define FRM_FLAG_HW_MATH 0x10u      /* OPT-IN, NOT BIT-EXACT: the Mandelbulb (scene 18) body, magnitude
+                                       and distance on the GPU's hardware transcendentals (v_log,
+                                       v_exp, v_sin, v_cos, v_sqrt, v_rcp), as a Vulkan driver lowers
+                                       fragment.wgsl's builtins (WGSL leaves their precision to the
+                                       implementation). Faster; frames differ from the oracle's and
+                                       are checked by the classified comparison against precise
+                                       builtins. Other scenes and the shading
+                                       are unchanged (exact). Never the default. */
 
 /* kernels (frm_kernel_for_pixels) */
 #define FRM_KERNEL_PERSISTENT 0u

@@ -67,3 +67,44 @@ def test_bands_reassemble_to_oracle_frame(gpu_renderer_factory, oracle, width, h
     finally:
         for rd in renderers:
             rd.close()
+
+
+@pytest.mark.parametrize("ranks,inflight", [(1, 1), (1, 2), (3, 2)])
+def test_moving_camera_reprojected_history_bit_exact(gpu_renderer_factory, oracle, ranks, inflight):
+    """A camera that moves every frame (frm.frame_sequence's fly-through, orbit sped up 20x so
+    the history lands pixels away) makes every launch project the previous launch's cost keys
+    into its camera (frm_sched.hip reproject_keys: hit points by their depth, misses by their
+    direction); whole frames (ranks = 1) and interleaved bands of 3 ranks reassembled: every
+    frame equals the oracle's render of its own Parameters."""
+    import torch
+
+    w = frm.WORKLOADS["HEADLINE_FLY"]
+    width, height, band_rows = 192, 108, 8
+    seq = frm.frame_sequence(w, pose="P1", dt=20 * frm.FRAME_SECONDS)
+    dev = torch.device("cuda", 0)
+    stride_rows = max(local_rows(height, band_rows, r, ranks) for r in range(ranks))
+    rank_stride = stride_rows * width * 4
+    gathered = torch.zeros(ranks * rank_stride, dtype=torch.uint8, device=dev)
+    out = torch.zeros(width * height * 4, dtype=torch.uint8, device=dev)
+    rds = [frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL, frames_in_flight=inflight)
+           for _ in range(ranks)]
+    try:
+        for frame in range(5):
+            p = next(seq)
+            for r, rd in enumerate(rds):
+                if frame == 0:
+                    rd.resize(width, height)
+                rd.update_parameters_buffer(p)
+                view = gathered[r * rank_stride:(r + 1) * rank_stride]
+                rd.render_bands(view.data_ptr(), rank_stride, band_rows if ranks > 1 else height, r, ranks, 0)
+            torch.cuda.synchronize()  # the ranks' context streams, before the reassembly reads them
+            if ranks > 1:
+                rds[0].unshuffle_bands(gathered.data_ptr(), rank_stride, out.data_ptr(), out.numel(), band_rows, ranks)
+            else:
+                out.copy_(gathered[:out.numel()])
+            torch.cuda.synchronize()
+            img = out.cpu().numpy().reshape(height, width, 4)
+            assert np.array_equal(img, oracle.render(p, width, height, 256)["rgba"]), f"frame {frame}"
+    finally:
+        for rd in rds:
+            rd.close()
