@@ -80,6 +80,10 @@ def parse():
                     help="frames per launch (frm_render_bands_batch: the frames' pixels share one work "
                     "queue, so a launch's tail is paid once per batch); 0 = auto (DESIGN.md section 7); "
                     "animated workloads (a new time every frame) always 1")
+    ap.add_argument("--math", default="exact", choices=["exact", "hw"],
+                    help="exact: the bit-exact frm builtins (the product default, the headline); hw: "
+                    "FRM_FLAG_HW_MATH, the Mandelbulb on hardware transcendentals (opt-in, not bit-exact, "
+                    "gated by tests/test_gpu_hw_math.py; a separate line, never the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in loop measurement (dropin_ms_per_frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -329,7 +333,8 @@ def main():
     params = next(seq)
     frame0 = params
     flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
-        {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel])
+        {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel]) | (
+        frm.FRM_FLAG_HW_MATH if args.math == "hw" else 0)
     split = 1 if (world == 1 or afr) else world  # ranks sharing one frame
     band_rows = args.band_rows or (w.height if split == 1 else tiling.choose_band_rows(w.height, world))
     local_pixels = w.width * min(w.height, tiling.rank_rows(w.height, band_rows, 0 if split == 1 else rank, split))
@@ -356,7 +361,10 @@ def main():
     elif batch > 1:
         inflight = 2 if split > 1 else 1
     else:
-        inflight = 3 if split > 1 or local_pixels < 4_000_000 else 2
+        # moving frames (a new time / camera every frame): the previous frame's cost keys do not
+        # predict the costliest pixels, so frames overlap more of each
+        # other's tail: 3 in flight (HEADLINE_FLY 11.61 / 11.37 / 11.51 ms at 2 / 3 / 4)
+        inflight = 3 if split > 1 or local_pixels < 4_000_000 or w.moving else 2
     inflight = max(1, min(inflight, frm.FRM_MAX_FRAMES_IN_FLIGHT))
     # exactly --steps timed and --warmup untimed frames: launches of `batch` frames, the last one
     # of each run takes the remainder (RowTiledFrame.run)
@@ -483,6 +491,9 @@ def main():
                 "workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
                 "num_iterations": w.iters, "max_steps": w.max_steps, "time": w.time,
                 "pose": args.pose, "frames_in_flight": inflight, "frames_per_launch": batch,
+                "math": ("exact (frm builtins, bit-exact with the oracle)" if args.math == "exact" else
+                         "hw (FRM_FLAG_HW_MATH: hardware transcendentals, NOT bit-exact; P1-classified, "
+                         "tests/test_gpu_hw_math.py)"),
                 "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "kernel": kernel_used + (" (runtime-compiled)" if args.reload else ""),
                 "animated": motion(w) if w.moving else False,
                 "parallelism": (f"row-bands x{world} (band_rows={band_rows}) + "
@@ -526,7 +537,11 @@ def main():
             out["comm"] = {"backend": backend, "ranks": comm_ranks,
                            "data_path": "dist.gather of row bands to rank 0" if split > 1 else "none (timing only)"}
             out["rccl_ranks"] = comm_ranks if backend == "nccl" else None
-        out.update(frame_check(first, args.workload, args.pose))
+        if args.math == "exact":
+            out.update(frame_check(first, args.workload, args.pose))
+        else:  # no golden: the hardware-math frame differs from the oracle's by design
+            out.update({"frame_sha256": hashlib.sha256(first.cpu().numpy().tobytes()).hexdigest(),
+                        "frame_sha_ok": None, "frame_golden": "none (FRM_FLAG_HW_MATH is not bit-exact)"})
         if dropin:
             out.update(dropin)
         if world == 1 and not args.no_cpu_baseline:

@@ -21,10 +21,6 @@ using namespace frm;
 // Mandelbulb persistent kernel: lanes that must be waiting before a wave runs its service
 // pass (tuning knob; FRM_SERVICE_MIN overrides it for experiments).
 static constexpr uint32_t kDefaultServiceMin = 24;  // swept 16..36 on MI355X (round 1: 20); round-2 kernel: headline 16/20/24/28 = 11.43/11.36/11.18/11.24 ms, C2 flat
-// Persistent kernel: a wave whose lane has spent this many cost units (Mandelbulb bodies, DEs
-// for the other families) on its current pixel runs at raised issue priority (s_setprio) until it
-// holds no such pixel. FRM_PRIO_COST overrides it (0 = off).
-static constexpr uint32_t kDefaultPrioCost = 0;
 // Kernel choice without a FRM_FLAG_*_KERNEL flag: below one resident persistent grid
 // (6 blocks of 256 lanes per CU for the Mandelbulb) a launch has fewer pixels than lanes,
 // and the persistent kernel's fixed costs (pixel sort, grid, separate shading pass) outweigh
@@ -61,11 +57,6 @@ struct Slot {
   // this slot's next launch, which rewrites them, waits for that copy
   hipEvent_t keys_read = nullptr;
   hipStream_t keys_reader = nullptr;
-  // the launch the keys come from: its last frame's camera and records (reprojection when the
-  // next launch's camera differs, frm_sched.hip reproject_keys)
-  FrameUniforms sched_f{};
-  size_t sched_rec_base = 0;
-  bool sched_records = false;
 };
 
 struct frm_ctx {
@@ -85,8 +76,6 @@ struct frm_ctx {
   size_t present_cap = 0;
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   uint32_t service_min = kDefaultServiceMin;
-  uint32_t prio_cost = kDefaultPrioCost;
-  bool reproject = true;  // FRM_NO_REPROJECT=1 turns the key reprojection off (A/B experiments)
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
@@ -178,7 +167,6 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.counters = counters;
   a.npix = band_valid_rows(ctx->height, a.g) * ctx->width;
   a.service_min = ctx->service_min;
-  a.prio_cost = ctx->prio_cost;
   a.batch = 1;
   a.rec_stride = local_rows * ctx->width;
   a.out_stride = local_rows * ctx->width;
@@ -236,7 +224,6 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   if (kind == kKernelPersistent) {
     const size_t need = (size_t)a.g.local_rows * a.f.width * a.batch;
     if (need > sl.records_cap) {  // grows outside the steady state (first frame of a size)
-      sl.sched_records = false;  // the records the keys came from are gone
       int rc = wait_slot(ctx, sl);
       if (rc) return rc;
       if (sl.records) FRM_HIP(ctx, hipFree(sl.records));
@@ -302,24 +289,6 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       dn.keys_reader = s;
     }
     const bool history = same || rescale || donor >= 0;
-    // the keys' frame was seen from another camera: project them into this launch's
-    FrameUniforms nf = a.f;
-    if (a.batch > 1) {
-      memcpy(nf.row, a.cams[0].row, sizeof(nf.row));
-      nf.origin = a.cams[0].origin;
-    }
-    if (same && sl.sched_records && ctx->reproject &&
-        (memcmp(nf.row, sl.sched_f.row, sizeof(nf.row)) != 0 || memcmp(&nf.origin, &sl.sched_f.origin, sizeof(v3)) != 0)) {
-      ReprojectArgs ra;
-      ra.prev = sl.sched_f;
-      ra.next = nf;
-      ra.g = a.g;
-      ra.tails = a.tails + sl.sched_rec_base;
-      ra.geom = a.geom + sl.sched_rec_base;
-      ra.npix = npix;
-      ra.valid_rows = npix / a.f.width;
-      FRM_HIP(ctx, reproject_keys(ra, sl.sched_keys, sl.sched_order, s));
-    }
     FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
                                  sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
     a.pixel_order = sl.sched_order;
@@ -329,9 +298,6 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
     sl.sched_whole = whole;
     sl.sched_w = a.f.width;
     sl.sched_h = a.f.height;
-    sl.sched_f = a.f;  // the keys shade_pass records are the last frame's (a.f = its camera)
-    sl.sched_rec_base = (size_t)(a.batch - 1u) * a.rec_stride;
-    sl.sched_records = true;
     a.debug = (unsigned long long*)(sl.queue + 8);  // bytes 32..71 of the queue block
     FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, sizeof(unsigned int), s));
 #ifdef FRM_STAMPS
@@ -732,6 +698,32 @@ int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
   if (rc) return rc;
   if (sl.keys_reader) FRM_HIP(ctx, hipEventSynchronize(sl.keys_read));
   FRM_HIP(ctx, hipMemcpy(sl.sched_keys, keys, n, hipMemcpyHostToDevice));
+  return FRM_OK;
+}
+
+// per-pixel shading inputs of the last frm_render (a whole persistent frame of the current size
+// and parameters): 10 floats per pixel, row-major, as the oracle's om_render_trace
+int frm_debug_trace(frm_ctx* ctx, float* out, size_t n_floats) {
+  int rc = ensure_ready(ctx);
+  if (rc) return rc;
+  if (!out) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "out is NULL");
+  const size_t npix = (size_t)ctx->width * ctx->height;
+  if (n_floats < npix * 10u)
+    return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "out holds %zu floats, the trace needs %zu", n_floats, npix * 10u);
+  const Slot& sl = ctx->slots[ctx->last_slot];
+  if (!sl.records || sl.records_cap < npix || !sl.sched_whole || sl.sched_w != ctx->width || sl.sched_h != ctx->height)
+    return fail(ctx, FRM_ERR_NOT_READY, "the last frm_render was not a persistent launch of this frame size");
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  KernelArgs a = make_args(ctx, sl.fb, ctx->counters, ctx->height, 0, 1, ctx->height);
+  a.geom = reinterpret_cast<ShadeGeom*>(sl.records);
+  a.tails = reinterpret_cast<ShadeTail*>(sl.records + sl.records_cap * sizeof(ShadeGeom));
+  float* d = nullptr;
+  FRM_HIP(ctx, hipMalloc(&d, npix * 10u * sizeof(float)));
+  hipError_t e = launch_trace(a, d, sl.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, npix * 10u * sizeof(float), hipMemcpyDeviceToHost, sl.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sl.stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "frm_debug_trace");
   return FRM_OK;
 }
 

@@ -47,9 +47,6 @@ struct KernelArgs {
   ShadeTail* tails;               // persistent kernel: local_rows * width march-end records
   uint32_t npix;                  // persistent kernel: pixels of the launch (= fetch positions)
   uint32_t service_min;           // persistent kernel: lanes waiting before a service pass
-  uint32_t prio_cost;             // persistent kernel: a wave holding a pixel that has run this many
-                                  // cost units (Mandelbulb bodies / DEs) issues at raised priority
-                                  // (0: never)
   unsigned long long* debug;      // diagnostic builds only (FRM_STAMPS): 5 x u64
   const uint32_t* pixel_order;    // persistent kernel: local pixel index at each fetch position
   uint8_t* pixel_key;             // persistent kernel: cost key per local pixel (out)
@@ -62,18 +59,6 @@ struct KernelArgs {
   uint32_t rec_stride;            // records per frame
   uint32_t out_stride;            // packed RGBA8 words per frame
   FrameCamera cams[kMaxBatch];
-};
-
-// Forward projection of the previous launch's cost keys into a moved camera (frm_sched.hip):
-// the records and camera of the launch whose keys the slot holds (its last frame), the camera
-// of the next launch's first frame, and the (unchanged) band geometry.
-struct ReprojectArgs {
-  FrameUniforms prev, next;
-  BandGeometry g;
-  const ShadeTail* tails;  // the previous launch's last frame's records
-  const ShadeGeom* geom;
-  uint32_t npix;           // local pixels (= valid_rows * width)
-  uint32_t valid_rows;
 };
 
 #ifndef FRM_MARCH_BLOCK
@@ -113,9 +98,6 @@ hipError_t schedule_pixels(uint32_t npix, bool has_history, const uint8_t* key, 
                            const uint32_t* iota, uint32_t* order, void* temp, size_t temp_bytes,
                            hipStream_t stream);
 hipError_t fill_iota(uint32_t* out, uint32_t n, hipStream_t stream);
-// Forward projection of keys (npix local pixels) from a.prev's camera into a.next's; scratch holds
-// npix u32 (the fetch order array, rewritten by the sort afterwards).
-hipError_t reproject_keys(const ReprojectArgs& a, uint8_t* keys, uint32_t* scratch, hipStream_t stream);
 // Whole-frame key map sw x sh -> dw x dh, nearest neighbour (history across a resize).
 hipError_t rescale_keys(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                         hipStream_t stream);
@@ -123,6 +105,8 @@ size_t schedule_temp_bytes(uint32_t npix);
 hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t n, float* dist, float* color,
                              hipStream_t stream);
 hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, float* out, hipStream_t stream);
+// 10 floats per local pixel from a persistent launch's records (frm_debug_trace)
+hipError_t launch_trace(const KernelArgs& a, float* out, hipStream_t stream);
 
 #endif  // !__HIPCC_RTC__
 

@@ -102,6 +102,45 @@ hipError_t launch_eval_scene(const SceneUniforms& s, const float* pts, uint32_t 
   return hipGetLastError();
 }
 
+// Per-pixel trace of the geometric inputs of the shading, from the records of a persistent launch
+// (parity tooling, frm_debug_trace; the layout of the oracle's om_render_trace): hit, primary
+// steps, normal xyz, sun hit, sun closeness, object colour xyz (hits), zeros for misses.
+template <uint32_t FAM>
+__global__ __launch_bounds__(256) void trace_pass(KernelArgs a, float* __restrict__ out) {
+  const uint32_t width = a.f.width;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= a.npix) return;
+  const uint32_t lr = idx / width, x = idx - lr * width;
+  const uint32_t y = band_row_to_global(a.g, lr);
+  const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[idx]);
+  float t[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (r1.y & kRecHit) {
+    const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[idx]);
+    const v3 hp = ray_at(a.f.origin, r0.x, camera_ray(a.f, x, y));
+    const v3 c = scene_color<FAM>(hp);
+    t[0] = 1.f;
+    t[1] = (float)(r1.y & kRecStepsMask);
+    t[2] = r0.y, t[3] = r0.z, t[4] = r0.w;
+    t[5] = (r1.y & kRecSunMiss) ? 0.f : 1.f;
+    t[6] = __uint_as_float(r1.x);
+    t[7] = c.x, t[8] = c.y, t[9] = c.z;
+  }
+  for (int k = 0; k < 10; ++k) out[(size_t)idx * 10u + k] = t[k];
+}
+
+hipError_t launch_trace(const KernelArgs& a, float* out, hipStream_t stream) {
+  const dim3 grid((a.npix + 255u) / 256u);
+  switch (a.s.family) {
+    case kMenger: hipLaunchKernelGGL(trace_pass<kMenger>, grid, dim3(256), 0, stream, a, out); break;
+    case kSierpinski: hipLaunchKernelGGL(trace_pass<kSierpinski>, grid, dim3(256), 0, stream, a, out); break;
+    case kKoch: hipLaunchKernelGGL(trace_pass<kKoch>, grid, dim3(256), 0, stream, a, out); break;
+    case kMandelbulb: hipLaunchKernelGGL(trace_pass<kMandelbulb>, grid, dim3(256), 0, stream, a, out); break;
+    case kMandelbulbHw: hipLaunchKernelGGL(trace_pass<kMandelbulbHw>, grid, dim3(256), 0, stream, a, out); break;
+    default: hipLaunchKernelGGL(trace_pass<kSphere>, grid, dim3(256), 0, stream, a, out); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_eval_math(int fn, const float* a, const float* b, uint32_t n, float* out, hipStream_t stream) {
   hipLaunchKernelGGL(eval_math, dim3((n + 255u) / 256u), dim3(256), 0, stream, fn, a, b, n, out);
   return hipGetLastError();

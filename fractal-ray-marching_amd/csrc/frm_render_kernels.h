@@ -121,7 +121,6 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   // wave-uniform state: current chunk of 64 fetched pixels, how many were handed out
   uint32_t slots_used = kChunk;
   bool exhausted = false;
-  bool raised = false;  // wave priority raised (a lane holds a long-running pixel)
   uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
 #ifdef FRM_COUNT_EXACT
   uint64_t n_dbg_total = 0, n_dbg_exact = 0;
@@ -358,19 +357,6 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
         de = scene_de<FAM, ITERS>(su, q, unused);
         done = true;
         pix_cost++;  // fixed-trip families: the scheduling cost unit is one DE
-      }
-    }
-
-    // a pixel whose march has already run long is likely the frame's critical path: its wave
-    // issues first among the SIMD's waves while it holds one (scheduling only, same bytes)
-    if (a.prio_cost) {
-      const bool hot = ballot(pix != kIdle && pix_cost >= a.prio_cost) != 0;
-      if (hot != raised) {
-        if (hot)
-          __builtin_amdgcn_s_setprio(3);
-        else
-          __builtin_amdgcn_s_setprio(0);
-        raised = hot;
       }
     }
 

@@ -32,6 +32,7 @@ FRM_FLAG_SCENE_SPHERE = 0x1
 FRM_FLAG_SIMPLE_KERNEL = 0x2
 FRM_FLAG_PERSISTENT_KERNEL = 0x4
 FRM_FLAG_UNBOUNDED_ITERATIONS = 0x8
+FRM_FLAG_HW_MATH = 0x10
 FRM_KERNEL_PERSISTENT = 0
 FRM_KERNEL_SIMPLE = 1
 FRM_BLIT_SRGB = 0x1
@@ -135,6 +136,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     ("frm_debug_pixel_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_debug_set_pixel_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("frm_debug_trace", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("frm_parameters_default", None, [_P(FrmParameters)]),
     ("frm_parameters_update_aspect", None, [_P(FrmParameters), ctypes.c_uint32, ctypes.c_uint32]),
     ("frm_parameters_update_time", None, [_P(FrmParameters), ctypes.c_float]),

@@ -164,6 +164,13 @@ class Renderer:
         k = np.ascontiguousarray(keys, dtype=np.uint8)
         self._check(self._lib.frm_debug_set_pixel_keys(self.ctx, k.ctypes.data, k.size))
 
+    def trace(self):
+        """frm_debug_trace: the shading inputs of every pixel of the last render, (H, W, 10) float32
+        in the oracle's trace layout (hit, steps, normal xyz, sun hit, sun closeness, colour xyz)."""
+        out = np.zeros((self.height, self.width, 10), np.float32)
+        self._check(self._lib.frm_debug_trace(self.ctx, out.ctypes.data, out.size))
+        return out
+
     def stats_from_counters(self, counters):
         arr = (ctypes.c_uint64 * _lib.FRM_NUM_COUNTERS)(*[int(c) for c in counters])
         st = _lib.FrmStats()

@@ -284,6 +284,13 @@ int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n);
  * (n = width x height; the next slot must hold a whole frame of the current size). */
 int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n);
 
+/* frm_debug_trace: the geometric inputs of the shading of every pixel of the last frm_render (a
+ * whole frame on the persistent kernel, the context's current size and parameters), 10 floats per
+ * pixel, row-major, in the layout of the oracle's per-pixel trace: hit, primary steps, normal xyz,
+ * sun hit, sun closeness, object colour xyz (hits; zeros for misses). Parity tooling for frames
+ * that are not bit-exact by design (FRM_FLAG_HW_MATH). n_floats >= 10 x width x height. */
+int frm_debug_trace(frm_ctx* ctx, float* out, size_t n_floats);
+
 /* ---- host-side mirrors of the reference's Parameters mutators (src/parameters.rs).
  *      These let a C/C++/Python host drive the same uniform without Rust. */
 void frm_parameters_default(frm_parameters* p);                               /* #[derive(Default)] */

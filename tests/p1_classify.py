@@ -103,3 +103,67 @@ def classify(oracle, params, width, height, max_steps, flags=0, threads=None):
         "march_steps_libm": int(b["counters"][2] + b["counters"][3]),
         **stats,
     }
+
+
+def trace_info(oracle, trace):
+    """The oracle's per-pixel info word (flags + primary steps << 8) rebuilt from a trace, for a
+    frame that has a trace but no oracle render (a GPU frame, frm_debug_trace)."""
+    t = trace.reshape(-1, 10)
+    hit = t[:, 0] != 0
+    cl = t[:, 6]
+    info = np.where(hit, oracle.INFO_HIT, 0)
+    info |= np.where(hit & (t[:, 5] != 0), oracle.INFO_SUN_HIT, 0)
+    info |= np.where(hit & (np.isnan(cl) | (cl == -np.inf)), oracle.INFO_SHADOW_FIRST_NONPOS, 0)
+    info |= np.where(hit & np.isnan(t[:, 2]), oracle.INFO_ZERO_NORMAL, 0)
+    return (info | (t[:, 1].astype(np.int64) << 8)).astype(np.int64)
+
+
+def classify_frame(oracle, params, width, height, max_steps, rgba, trace, flags=0, threads=None):
+    """classify() for a frame that is not the oracle's own (e.g. the GPU's FRM_FLAG_HW_MATH frame,
+    with its trace from frm_debug_trace) against the MODE_LIBM oracle: first, the frame's trace
+    re-shaded with the frm shading reproduces the frame's bytes exactly (`trace_reproduces`:
+    every difference is then geometric, none comes from the shading or the encode); then the same
+    classes and the same `unexplained` count as classify()."""
+    b = oracle.render(params, width, height, max_steps, flags=flags, mode=oracle.MODE_LIBM, threads=threads,
+                      info=True, trace=True)
+    ys, xs = np.mgrid[0:height, 0:width]
+    xs, ys = xs.ravel(), ys.ravel()
+    ra, rb = rgba.reshape(-1, 4), b["rgba"].reshape(-1, 4)
+    ta, tb = trace.reshape(-1, 10).astype(np.float32), b["trace"].reshape(-1, 10)
+    ia, ib = trace_info(oracle, trace), b["info"].ravel().astype(np.int64)
+    own_a = oracle.shade_trace(params, width, height, max_steps, xs, ys, ta, flags=flags)
+    reproduces = int(np.sum(np.any(own_a != ra, -1)))
+    frm_on_libm = oracle.shade_trace(params, width, height, max_steps, xs, ys, tb, flags=flags)
+    shading_ok = _within1(frm_on_libm, rb)
+    diff = ~_within1(ra, rb)
+    idx = np.nonzero(diff)[0]
+    cls = np.full(idx.size, "", dtype=object)
+    fa, fb = ia[idx], ib[idx]
+    rules = [
+        ("hit_miss_flip", ((fa ^ fb) & oracle.INFO_HIT) != 0),
+        ("shadow_first_nonpositive", ((fa | fb) & oracle.INFO_SHADOW_FIRST_NONPOS) != 0),
+        ("zero_normal", ((fa | fb) & oracle.INFO_ZERO_NORMAL) != 0),
+        ("sun_hit_flip", ((fa ^ fb) & oracle.INFO_SUN_HIT) != 0),
+        ("ao_step_count", (fa >> 8) != (fb >> 8)),
+    ]
+    for name, m in rules:
+        cls[(cls == "") & m] = name
+    rest = np.nonzero(cls == "")[0]
+    if rest.size:
+        p = idx[rest]
+        for name, sl in SUBST:
+            t = ta[p].copy()
+            t[:, sl] = tb[p][:, sl]
+            ok = _within1(oracle.shade_trace(params, width, height, max_steps, xs[p], ys[p], t, flags=flags), rb[p])
+            sel = ok & (cls[rest] == "")
+            cls[rest[sel]] = name
+        cls[cls == ""] = "several"
+    return {
+        "width": width, "height": height, "pixels": width * height,
+        "trace_mismatch_pixels": reproduces,
+        "differ_gt1": int(idx.size), "differ_gt1_frac": idx.size / (width * height),
+        "differ_any": int(np.sum(np.any(ra[:, :3] != rb[:, :3], -1))),
+        "classes": {k: int(np.sum(cls == k)) for k in CLASSES},
+        "unexplained": int(np.sum(~shading_ok[idx])),
+        "march_steps_libm": int(b["counters"][2] + b["counters"][3]),
+    }

@@ -70,12 +70,11 @@ def test_bands_reassemble_to_oracle_frame(gpu_renderer_factory, oracle, width, h
 
 
 @pytest.mark.parametrize("ranks,inflight", [(1, 1), (1, 2), (3, 2)])
-def test_moving_camera_reprojected_history_bit_exact(gpu_renderer_factory, oracle, ranks, inflight):
-    """A camera that moves every frame (frm.frame_sequence's fly-through, orbit sped up 20x so
-    the history lands pixels away) makes every launch project the previous launch's cost keys
-    into its camera (frm_sched.hip reproject_keys: hit points by their depth, misses by their
-    direction); whole frames (ranks = 1) and interleaved bands of 3 ranks reassembled: every
-    frame equals the oracle's render of its own Parameters."""
+def test_moving_camera_history_bit_exact(gpu_renderer_factory, oracle, ranks, inflight):
+    """A camera and a time that move every frame (frm.frame_sequence's fly-through, sped up 20x)
+    so every launch fetches its pixels in the order of another frame's cost keys; whole frames
+    (ranks = 1) and interleaved bands of 3 ranks reassembled: every frame equals the oracle's
+    render of its own Parameters."""
     import torch
 
     w = frm.WORKLOADS["HEADLINE_FLY"]
