@@ -163,23 +163,27 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       const uint64_t waitable = exhausted ? live : ~0ull;
       for (;;) {
         if (pending == 0 || (uint32_t)__popcll(waitable & ~pending) >= a.service_min) break;
-        n_body += (uint64_t)__popcll(pending);  // one body per computing lane this iteration
+        // one iteration per computing lane; an iteration that bails out runs no body, so the
+        // frame's bodies are iterations - bailouts (n_bail, counted when the DE is consumed)
+        n_body += (uint64_t)__popcll(pending);
 #ifdef FRM_STAMPS
         n_loop++;
 #endif
         uint32_t fin = 0;
         if (lane_in(pending)) {
-#if defined(FRM_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostic: body-loop iterations, and those that ran the exact body
-          n_dbg_total++;
-          if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
-#endif
-          mb_step<kHw>(su, q, mag, z, dr);
-          body++;
-          if (body > n_iter) {
-            fin = 1;  // N+1 bodies: the distance uses the last loop-top magnitude
+          // one iteration of fragment.wgsl:245-267: the loop-top magnitude, the bailout test,
+          // then one body (a DE starts here with z = its sample point, body = 0)
+          mag = mb_length<kHw>(z);
+          if (mag > su.mb_bailout) {
+            fin = 1;  // bailout: no body this iteration (n_bail corrects the body count)
           } else {
-            mag = mb_length<kHw>(z);
-            fin = mag > su.mb_bailout;
+#if defined(FRM_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostic: body-loop iterations, and those that ran the exact body
+            n_dbg_total++;
+            if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
+#endif
+            mb_step<kHw>(su, q, mag, z, dr);
+            body++;
+            fin = body > n_iter;  // N+1 bodies: the distance uses this iteration's magnitude
           }
         }
         pending &= ~ballot(fin != 0);
@@ -346,12 +350,11 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       const float e = kMinDistance;
       const float ex = (kq == 0u || kq == 3u) ? e : -e, ey = (kq >= 2u) ? e : -e, ez = (kq == 1u || kq == 3u) ? e : -e;
       q = mk(is_tap ? r.x + ex : r.x, is_tap ? r.y + ey : r.y, is_tap ? r.z + ez : r.z);
-      if constexpr (kMb) {
+      if constexpr (kMb) {  // the body loop takes the magnitude and the bailout test
         z = q;
         dr = 1.f;
         body = 0;
-        mag = mb_length<kHw>(q);
-        done = mag > su.mb_bailout;
+        done = false;
       } else {
         DeCount unused = {0u, 0u};
         de = scene_de<FAM, ITERS>(su, q, unused);
@@ -405,6 +408,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 #ifdef FRM_COUNT_EXACT
     atomicAdd(&a.counters[7], (unsigned long long)((n_dbg_total << 32) | n_dbg_exact));
 #endif
+    if constexpr (kMb) n_body -= n_bail;  // loop iterations that bailed out ran no body
     unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll
     for (int k = 0; k < 7; ++k)
