@@ -43,7 +43,10 @@ def frames_per_dispatch(d):
     for n in ("sq", "wr", "rd", "sq2"):
         try:
             with open(f"{d}/{n}.json") as fh:
-                return int(json.loads(fh.read().strip().splitlines()[-1])["config"].get("frames_per_launch", 1))
+                line = json.loads(fh.read().strip().splitlines()[-1])
+                if "config" in line:  # a bench.py line
+                    return int(line["config"].get("frames_per_launch", 1))
+                return int(line.get("batch", 1))  # a tools/pipeline_probe.py line
         except (OSError, ValueError, KeyError, IndexError):
             continue
     return 1
