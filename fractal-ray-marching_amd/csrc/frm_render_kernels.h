@@ -171,19 +171,17 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 #endif
         uint32_t fin = 0;
         if (lane_in(pending)) {
-          // one iteration of fragment.wgsl:245-267: the loop-top magnitude, the bailout test,
-          // then one body (a DE starts here with z = its sample point, body = 0)
-          mag = mb_length<kHw>(z);
-          if (mag > su.mb_bailout) {
-            fin = 1;  // bailout: no body this iteration (n_bail corrects the body count)
-          } else {
 #if defined(FRM_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostic: body-loop iterations, and those that ran the exact body
-            n_dbg_total++;
-            if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
+          n_dbg_total++;
+          if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
 #endif
-            mb_step<kHw>(su, q, mag, z, dr);
-            body++;
-            fin = body > n_iter;  // N+1 bodies: the distance uses this iteration's magnitude
+          mb_step<kHw>(su, q, mag, z, dr);
+          body++;
+          if (body > n_iter) {
+            fin = 1;  // N+1 bodies: the distance uses the last loop-top magnitude
+          } else {
+            mag = mb_length<kHw>(z);
+            fin = mag > su.mb_bailout;
           }
         }
         pending &= ~ballot(fin != 0);
@@ -350,11 +348,12 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       const float e = kMinDistance;
       const float ex = (kq == 0u || kq == 3u) ? e : -e, ey = (kq >= 2u) ? e : -e, ez = (kq == 1u || kq == 3u) ? e : -e;
       q = mk(is_tap ? r.x + ex : r.x, is_tap ? r.y + ey : r.y, is_tap ? r.z + ez : r.z);
-      if constexpr (kMb) {  // the body loop takes the magnitude and the bailout test
+      if constexpr (kMb) {
         z = q;
         dr = 1.f;
         body = 0;
-        done = false;
+        mag = mb_length<kHw>(q);
+        done = mag > su.mb_bailout;
       } else {
         DeCount unused = {0u, 0u};
         de = scene_de<FAM, ITERS>(su, q, unused);
