@@ -156,7 +156,8 @@ def pmc_summary(workload, world):
     cur = provenance.source_sha256()
     stale = None
     tag = workload if world == 1 else f"{workload}_share{world}"
-    for rnd in ("round3", "round2", "round1"):
+    for rnd in sorted((d for d in os.listdir(os.path.join(ROOT, "profiles")) if d.startswith("round")),
+                      key=lambda d: int(d[5:]) if d[5:].isdigit() else -1, reverse=True):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_march.json")
         if not os.path.exists(path):
             continue
@@ -280,6 +281,30 @@ def frame_check(frame, workload, pose):
             "frame_golden": None if gold is None else f"tests/golden/fullsize.json[{key}]"}
 
 
+COUNTER_NAMES = ("pixels", "hit_pixels", "primary_steps", "shadow_steps", "normal_evals", "fractal_bodies",
+                 "fractal_bailouts")
+
+
+def counters_check(counters, workload, pose, frames, golden_path=GOLDEN):
+    """The kernel's summed work counters of the timed region against `frames` x the oracle's
+    counters of the golden frame (tests/golden/fullsize.json). The roofline's algorithmic ops
+    are derived from these counters (fractal bodies and bailouts are data dependent) and the
+    frame hash cannot see them, so a wrong count must not reach the line. Applies when every
+    timed frame is the golden frame (fixed workloads; all ranks of a row split together);
+    returns None when it does not apply, else {"counters_ok": bool, ...}."""
+    gold = None
+    if os.path.exists(golden_path):
+        with open(golden_path) as fh:
+            gold = json.load(fh).get(f"{workload}_{pose}")
+    if gold is None:
+        return None
+    want = [frames * int(v) for v in gold["counters"][:len(COUNTER_NAMES)]]
+    got = [int(v) for v in counters[:len(COUNTER_NAMES)]]
+    bad = {n: {"got": g, "want": e} for n, g, e in zip(COUNTER_NAMES, got, want) if g != e}
+    return {"counters_ok": not bad, "counters_golden": f"{frames} x tests/golden/fullsize.json[{workload}_{pose}]",
+            **({"counters_mismatch": bad} if bad else {})}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -393,8 +418,8 @@ def main():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(s)
         if batch > 1:  # one launch, `count` frames (same scene and camera here), frame b at b * tf.nbytes
-            r.render_bands_batch([params] * count, buf.data_ptr(), tf.nbytes, br, first, stride, s.cuda_stream,
-                                 counters.data_ptr(), dst_bytes=buf.numel())
+            r.render_bands_batch([params] * count, buf.data_ptr(), buf.numel(), tf.nbytes, br, first, stride,
+                                 s.cuda_stream, counters.data_ptr())
         else:
             r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
         if ev is not None:
@@ -542,11 +567,25 @@ def main():
         else:  # no golden: the hardware-math frame differs from the oracle's by design
             out.update({"frame_sha256": hashlib.sha256(first.cpu().numpy().tobytes()).hexdigest(),
                         "frame_sha_ok": None, "frame_golden": "none (FRM_FLAG_HW_MATH is not bit-exact)"})
+        # every timed frame is frame 0 (fixed workloads; a row split's ranks sum to whole frames):
+        # the summed counters must be steps x the golden frame's, or the roofline is not reported
+        cc = None
+        if args.math == "exact" and not w.moving and not afr:
+            cc = counters_check(c, args.workload, args.pose, args.steps)
+        if cc is not None:
+            out.update(cc)
+            if not cc["counters_ok"]:
+                for k in ("achieved", "frac", "algorithmic_ops_per_frame"):
+                    out["roofline"][k] = None
         if dropin:
             out.update(dropin)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(params, w, args.cpu_seconds)
         print(json.dumps(out))
+        if cc is not None and not cc["counters_ok"]:
+            print(f"bench.py: work counters differ from the oracle's: {cc['counters_mismatch']}", file=sys.stderr)
+            r.close()
+            raise SystemExit(3)
     r.close()
     if world > 1:
         dist.destroy_process_group()

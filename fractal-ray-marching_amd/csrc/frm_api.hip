@@ -284,6 +284,9 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
     if (donor >= 0) {  // keys order fetches only, never a pixel's bytes
       Slot& dn = ctx->slots[donor];
       if (dn.pending && dn.last_stream != s) FRM_HIP(ctx, hipStreamWaitEvent(s, dn.done, 0));
+      // an earlier reader's copy on another stream: order this copy after it, so the one
+      // keys_read event recorded below covers every copy the donor's next launch must await
+      if (dn.keys_reader && dn.keys_reader != s) FRM_HIP(ctx, hipStreamWaitEvent(s, dn.keys_read, 0));
       FRM_HIP(ctx, hipMemcpyAsync(sl.sched_keys, dn.sched_keys, npix, hipMemcpyDeviceToDevice, s));
       FRM_HIP(ctx, hipEventRecord(dn.keys_read, s));  // the donor's next launch waits for this copy
       dn.keys_reader = s;
@@ -595,7 +598,9 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT,
                 "frame stride %zu: below a frame's %zu bytes, not a multiple of 4 or not below 16 GiB",
                 frame_stride_bytes, need);
-  if (dst_bytes < need || (dst_bytes - need) / frame_stride_bytes < count - 1u)
+  // a stride of 0 passes the check above only for a rank without bands (need == 0): its frames
+  // occupy no bytes
+  if (dst_bytes < need || (frame_stride_bytes != 0 && (dst_bytes - need) / frame_stride_bytes < count - 1u))
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, %u frames %zu bytes apart need %zu", dst_bytes,
                 count, frame_stride_bytes, (size_t)(count - 1u) * frame_stride_bytes + need);
   // fetch positions are u32 and every wave's last queue claims run up to two chunks past the

@@ -163,8 +163,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       const uint64_t waitable = exhausted ? live : ~0ull;
       for (;;) {
         if (pending == 0 || (uint32_t)__popcll(waitable & ~pending) >= a.service_min) break;
-        // one iteration per computing lane; an iteration that bails out runs no body, so the
-        // frame's bodies are iterations - bailouts (n_bail, counted when the DE is consumed)
+        // one body per computing lane this iteration (a DE that bails out at entry never
+        // becomes pending, so this counts bodies exactly: fragment.wgsl:245-249)
         n_body += (uint64_t)__popcll(pending);
 #ifdef FRM_STAMPS
         n_loop++;
@@ -407,7 +407,6 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 #ifdef FRM_COUNT_EXACT
     atomicAdd(&a.counters[7], (unsigned long long)((n_dbg_total << 32) | n_dbg_exact));
 #endif
-    if constexpr (kMb) n_body -= n_bail;  // loop iterations that bailed out ran no body
     unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll
     for (int k = 0; k < 7; ++k)

@@ -134,59 +134,31 @@ FRM_HD float tetrahedron(const SceneUniforms& u, v3 p) {
 // box (138-141), repeat (190-192), cross_inside (194-200). FAST (GPU, u.menger_fast): the
 // division by the scale uses the precomputed reciprocal (the next one is loaded an iteration
 // ahead); same bits.
-// One fold of menger_sponge (fragment.wgsl:207-209) at scale_i = scale.
-FRM_HD float menger_fold(const SceneUniforms& u, v3 p, float d, float scale, float rcp, bool fast) {
-  v3 r = p * scale;
-  v3 c = mk(fract_(r.x + 0.5f) - 0.5f, fract_(r.y + 0.5f) - 0.5f, fract_(r.z + 0.5f) - 0.5f);
-  v3 a = abs3(c);
-  float cx = max_(a.y, a.z), cy = max_(a.z, a.x), cz = max_(a.x, a.y);
-  float ci = min_(min_(cx, cy), cz) - u.menger_cross;
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (fast) return max_quiet(d, div_by_rcp(-ci, scale, rcp));
-#endif
-  (void)rcp;
-  (void)fast;
-  return max_(d, (-ci) / scale);
-}
-#if defined(__HIP_DEVICE_COMPILE__)
-// folds I.. of the fast path with constant reciprocal indices (template recursion: every
-// u.menger_rcp[I] is a fixed kernarg offset, loaded once into scalar registers instead of by a
-// scalar load in every fold that the fold then waits for); n <= kMengerFastMax (set_menger)
-template <uint32_t I>
-__device__ __forceinline__ float menger_folds_fast(const SceneUniforms& u, v3 p, float d, float scale, uint32_t n) {
-  if constexpr (I < kMengerFastMax) {
-    if (I >= n) return d;
-    d = menger_fold(u, p, d, scale, u.menger_rcp[I], true);
-    return menger_folds_fast<I + 1u>(u, p, d, scale * u.menger_factor, n);
-  } else {
-    return d;
-  }
-}
-#endif
 template <bool ITERS, bool FAST>
 FRM_HD float menger_folds(const SceneUniforms& u, v3 p, float d) {
   const uint32_t n = iterations<ITERS>(u.n);
-#if defined(__HIP_DEVICE_COMPILE__) && defined(FRM_MENGER_VRCP)  // A/B: Newton from v_rcp, no table
-  if constexpr (FAST) {
-    float scale = 1.0f;
-    for (uint32_t i = 0; i < n; ++i) {
-      v3 r = p * scale;
-      v3 c = mk(fract_(r.x + 0.5f) - 0.5f, fract_(r.y + 0.5f) - 0.5f, fract_(r.z + 0.5f) - 0.5f);
-      v3 a = abs3(c);
-      float cx = max_(a.y, a.z), cy = max_(a.z, a.x), cz = max_(a.x, a.y);
-      float ci = min_(min_(cx, cy), cz) - u.menger_cross;
-      d = max_quiet(d, div_tame(-ci, scale));
-      scale = scale * u.menger_factor;
-    }
-    return d;
-  }
-#elif defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (FAST) return menger_folds_fast<0u>(u, p, d, 1.0f, n);
-#endif
   float scale = 1.0f;
+  float rcp = FAST ? u.menger_rcp[0] : 0.0f;
   for (uint32_t i = 0; i < n; ++i) {
-    d = menger_fold(u, p, d, scale, 0.0f, false);
+    const float rcp_next = FAST ? u.menger_rcp[i + 1u < kMengerFastMax ? i + 1u : kMengerFastMax - 1u] : 0.0f;
+    v3 r = p * scale;
+    v3 c = mk(fract_(r.x + 0.5f) - 0.5f, fract_(r.y + 0.5f) - 0.5f, fract_(r.z + 0.5f) - 0.5f);
+    v3 a = abs3(c);
+    float cx = max_(a.y, a.z), cy = max_(a.z, a.x), cz = max_(a.x, a.y);
+    float ci = min_(min_(cx, cy), cz) - u.menger_cross;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float q = FAST ? div_by_rcp(-ci, scale, rcp) : (-ci) / scale;
+    if constexpr (FAST)
+      d = max_quiet(d, q);
+    else
+      d = max_(d, q);
+#else
+    (void)rcp;
+    const float q = (-ci) / scale;
+    d = max_(d, q);
+#endif
     scale = scale * u.menger_factor;
+    rcp = rcp_next;
   }
   return d;
 }

@@ -103,13 +103,12 @@ class Renderer:
         self._check(self._lib.frm_render_bands(self.ctx, dev_ptr, nbytes, band_rows, first_band,
                                                band_stride, stream or None, dev_counters or None))
 
-    def render_bands_batch(self, params_list, dev_ptr, frame_stride, band_rows, first_band, band_stride,
-                           stream=0, dev_counters=0, dst_bytes=None):
+    def render_bands_batch(self, params_list, dev_ptr, dst_bytes, frame_stride, band_rows, first_band, band_stride,
+                           stream=0, dev_counters=0):
         """frm_render_bands_batch: len(params_list) frames (same scene, camera may differ) in
         one launch, frame k at dev_ptr + k * frame_stride; dst_bytes = the size of the buffer at
-        dev_ptr (default: len(params_list) * frame_stride)."""
-        if dst_bytes is None:
-            dst_bytes = len(params_list) * frame_stride
+        dev_ptr (the library checks every frame against it: pass the real allocation, e.g.
+        tensor.numel(), never a size derived from the stride)."""
         from ._lib import FrmParameters
         arr = (FrmParameters * len(params_list))()
         for k, p in enumerate(params_list):

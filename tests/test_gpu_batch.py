@@ -34,7 +34,7 @@ def test_batch_whole_frames_bit_exact(frm_lib, oracle, scene, iters, steps, infl
         for rep in range(3):  # the second and third batches fetch in the scheduled order
             counters.zero_()
             out.zero_()
-            r.render_bands_batch(ps, out.data_ptr(), fb, h, 0, 1, 0, counters.data_ptr())
+            r.render_bands_batch(ps, out.data_ptr(), out.numel(), fb, h, 0, 1, 0, counters.data_ptr())
             torch.cuda.synchronize()
             img = out.cpu().numpy().reshape(len(ps), h, w, 4)
             for k, ref in enumerate(refs):
@@ -59,7 +59,7 @@ def test_batch_band_split_bit_exact(frm_lib, oracle):
         for rep in range(2):
             for rk, rd in enumerate(rds):
                 rd.resize(w, h)
-                rd.render_bands_batch(ps, gathered.data_ptr() + rk * B * nb, nb, br, rk, ranks)
+                rd.render_bands_batch(ps, gathered.data_ptr() + rk * B * nb, B * nb, nb, br, rk, ranks)
             torch.cuda.synchronize()
             for b, p in enumerate(ps):
                 frame = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
@@ -84,19 +84,19 @@ def test_batch_rejects_frames_that_differ_beyond_the_camera(frm_lib):
         r.resize(w, h)
         for other in (b, c):
             with pytest.raises(frm.FrmError) as e:
-                r.render_bands_batch([a, other], buf.data_ptr(), w * h * 4, h, 0, 1)
+                r.render_bands_batch([a, other], buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
             assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
         with pytest.raises(frm.FrmError):
-            r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), w * h * 4, h, 0, 1)
+            r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
         # the destination must hold every frame: (count - 1) strides + one frame
         for n, stride in ((2, w * h * 4 + 4), (3, w * h * 4)):
             with pytest.raises(frm.FrmError) as e:
-                r.render_bands_batch([a] * n, buf.data_ptr(), stride, h, 0, 1, dst_bytes=buf.numel())
+                r.render_bands_batch([a] * n, buf.data_ptr(), buf.numel(), stride, h, 0, 1)
             assert e.value.code == _lib.FRM_ERR_BUFFER_TOO_SMALL
         with pytest.raises(frm.FrmError) as e:  # strides of 16 GiB and more do not fit the kernel's word stride
-            r.render_bands_batch([a] * 2, buf.data_ptr(), 1 << 34, h, 0, 1, dst_bytes=1 << 35)
+            r.render_bands_batch([a] * 2, buf.data_ptr(), 1 << 35, 1 << 34, h, 0, 1)
         assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
-        r.render_bands_batch([a] * 2, buf.data_ptr(), w * h * 4, h, 0, 1, dst_bytes=buf.numel())
+        r.render_bands_batch([a] * 2, buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
 
 
 def test_batch_of_max_frames_two_slots(frm_lib, oracle):
@@ -118,9 +118,26 @@ def test_batch_of_max_frames_two_slots(frm_lib, oracle):
         r.resize(w, h)
         for rep in range(3):
             for o in outs:
-                r.render_bands_batch(ps, o.data_ptr(), fb, h, 0, 1, 0, counters.data_ptr())
+                r.render_bands_batch(ps, o.data_ptr(), o.numel(), fb, h, 0, 1, 0, counters.data_ptr())
             torch.cuda.synchronize()
             for j, o in enumerate(outs):
                 img = o.cpu().numpy().reshape(B, h, w, 4)
                 for k in range(B):
                     assert np.array_equal(img[k], refs[k % len(refs)]["rgba"]), f"rep {rep} launch {j} frame {k}"
+
+
+def test_batch_rank_without_bands(frm_lib):
+    """A rank that holds no band of the frame (rows == 0) renders nothing and succeeds, also
+    with a zero frame stride and a zero-byte destination (no division by the stride)."""
+    import torch
+
+    w, h, br, ranks = 32, 8, 8, 2  # one band: rank 1 has none
+    a = params_for(18, 12, frm.POWER8_TIME, w, h)
+    buf = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with frm.Renderer(device=0, max_steps=64) as r:
+        r.resize(w, h)
+        for stride in (0, 4):
+            r.render_bands_batch([a] * 3, buf.data_ptr(), 0, stride, br, 1, ranks, 0, counters.data_ptr())
+        torch.cuda.synchronize()
+        assert int(counters.sum()) == 0 and int(buf.sum()) == 0

@@ -181,8 +181,8 @@ def _split_frames(name, ranks, params_list, batch, inflight):
             for r, rd in enumerate(rds):
                 buf = gathered[r * n:(r + 1) * n]
                 if batch > 1:
-                    rd.render_bands_batch(ps, buf.data_ptr(), nbytes, band_rows, r, ranks, 0, counters.data_ptr(),
-                                          dst_bytes=n)
+                    rd.render_bands_batch(ps, buf.data_ptr(), buf.numel(), nbytes, band_rows, r, ranks, 0,
+                                          counters.data_ptr())
                 else:
                     rd.update_parameters_buffer(ps[0])
                     rd.render_bands(buf.data_ptr(), n, band_rows, r, ranks, 0, counters.data_ptr())

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-3 profile session (one gpurun call per PART; every GPU step has its own time limit and
-# the chain stops at the first failure). Outputs under $OUT, copied into profiles/round3/.
+# Profile session (one gpurun call per PART; every GPU step has its own time limit and
+# the chain stops at the first failure). Outputs under $OUT, copied into profiles/roundN/.
 #   PART=tests   pytest -m gpu, the default bench line (+ CPU baseline), its rocprofv3 kernel
 #                trace (--kernel-trace --stats) and per-frame span (rocprof_timed.py)
 #   PART=configs every BASELINE config + HEADLINE_FLY + the FRM_FLAG_HW_MATH line, one bench line each
 #   PART=pmc     PMC passes (tools/pmc.sh, one counter group per run) of the headline, C2-C5 and one
 #                rank's share of the 8-way headline split; summaries for march_persistent and shade_pass
 set -o pipefail
-OUT=${OUT:-gpurun_out/round3}
+OUT=${OUT:-gpurun_out/session}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 case "$PART" in
@@ -15,6 +15,8 @@ tests)
   (lscpu | head -20; nproc) > "$OUT/host.txt" 2>&1
   timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -1 "$OUT/pytest_gpu.log"
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail "$OUT/smoke.log"; exit 1; }
+  tail -1 "$OUT/smoke.log"
   timeout -k 10 400 python bench.py --steps 20 --warmup 5 > "$OUT/bench_HEADLINE.json" 2> "$OUT/bench.err" || { tail "$OUT/bench.err"; exit 1; }
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-dropin > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { tail "$OUT/prof.err"; exit 1; }
   python tools/rocprof_timed.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" 2 10 > "$OUT/rocprof_timed_HEADLINE.txt"

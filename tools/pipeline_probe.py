@@ -73,8 +73,8 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
             if events:
                 torch.cuda.Event(enable_timing=True).record(ss[i])
             if batch > 1:
-                rs[i].render_bands_batch([p] * batch, bufs[i].data_ptr(), fbytes, br, rank, ranks, ss[i].cuda_stream,
-                                         counters.data_ptr())
+                rs[i].render_bands_batch([p] * batch, bufs[i].data_ptr(), bufs[i].numel(), fbytes, br, rank, ranks,
+                                         ss[i].cuda_stream, counters.data_ptr())
             else:
                 rs[i].render_bands(bufs[i].data_ptr(), bufs[i].numel(), br, rank, ranks, ss[i].cuda_stream,
                                    counters.data_ptr())
