@@ -191,34 +191,56 @@ def pmc_summary(workload, world):
 
 
 def dropin_loop(frm, torch, w, args, flags, local, camera):
-    """The drop-in binding's frame loop, measured in the same run:
-    a context with frames_in_flight = 1, one frm_render per frame with that frame's
-    Parameters (frm.frame_sequence, as bench's timed region), and the host waiting for every
-    frame before the next (frm_render with stats: the reference presents every frame,
-    graphics.rs:91-110). Untimed: 2 frames of frame 0. Timed: min(--steps, 20) frames."""
+    """The drop-in binding's frame loop, measured in the same run: one
+    frm_render per frame with that frame's Parameters (frm.frame_sequence, as bench's timed
+    region), every frame read back to the host (the reference presents every frame,
+    graphics.rs:91-110). Two forms:
+    * dropin (the binding): frames_in_flight = 2 and presentation with a frame of latency, as the
+      reference's surface has it (wgpu's default desired_maximum_frame_latency = 2,
+      persistent_graphics.rs:158-162): render frame k, start its readback
+      (frm_read_frame_async), then wait for frame k-1's pixels (frm_frame_pixels);
+    * dropin_sync: frames_in_flight = 1 and a wait for every frame before the next.
+    Untimed: 2 frames of frame 0. Timed: min(--steps, 20) frames. The march steps come from a
+    second, untimed pass over the same frames with stats."""
     seq = frm.frame_sequence(w, pose=args.pose, camera=camera)
-    p0 = next(seq)
     n = max(1, min(args.steps, 20))
-    with frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=1) as r:
-        r.resize(w.width, w.height)
-        r.update_parameters_buffer(p0)
-        for _ in range(2):
-            r.render(stats=True)
-        steps = 0
-        kernel_ms = 0.0
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(n):
-            if k > 0 and w.moving:
-                r.update_parameters_buffer(next(seq))
-            st = r.render(stats=True)
-            steps += st["march_steps"]
-            kernel_ms += st["kernel_ms"]
-        dt = time.perf_counter() - t0
-    return {"dropin_ms_per_frame": dt / n * 1e3,
-            "dropin": {"frames": n, "value": steps / dt / 1e9, "unit": "Gray-march-steps/s",
-                       "kernel_ms_per_frame": kernel_ms / n, "frames_in_flight": 1, "frames_per_launch": 1,
-                       "loop": "frm_render(stats) per frame, host waits for each frame (INTEGRATION.md section 3)"}}
+    frames = [next(seq) for _ in range(n)] if w.moving else [next(seq)] * n
+    out = {}
+    for name, fif, lag in (("dropin", 2, 1), ("dropin_sync", 1, 0)):
+        with frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=fif) as r:
+            r.resize(w.width, w.height)
+            r.update_parameters_buffer(frames[0])
+            for _ in range(2):
+                r.render(stats=False)
+                r.frame_pixels(r.read_frame_async(), copy=False)
+            held = []
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(n):
+                r.update_parameters_buffer(frames[k])
+                r.render(stats=False)
+                held.append(r.read_frame_async())
+                if len(held) > lag:
+                    r.frame_pixels(held.pop(0), copy=False)  # present frame k - lag
+            for t in held:
+                r.frame_pixels(t, copy=False)
+            dt = time.perf_counter() - t0
+            if name == "dropin":
+                steps = kernel_ms = 0
+                for p in frames:
+                    r.update_parameters_buffer(p)
+                    st = r.render(stats=True)
+                    steps += st["march_steps"]
+                    kernel_ms += st["kernel_ms"]
+        out[f"{name}_ms_per_frame"] = dt / n * 1e3
+        out[name] = {"frames": n, "value": steps / dt / 1e9, "unit": "Gray-march-steps/s",
+                     "frames_in_flight": fif, "frames_per_launch": 1, "present_latency_frames": lag,
+                     "loop": ("frm_render + frm_read_frame_async per frame, frm_frame_pixels of the previous "
+                              "frame (INTEGRATION.md section 3)" if lag else
+                              "frm_render + readback per frame, host waits for each frame")}
+        if name == "dropin":
+            out[name]["kernel_ms_per_frame_alone"] = kernel_ms / n
+    return out
 
 
 def launch_ranks(args):

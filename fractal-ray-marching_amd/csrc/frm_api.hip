@@ -57,6 +57,16 @@ struct Slot {
   // this slot's next launch, which rewrites them, waits for that copy
   hipEvent_t keys_read = nullptr;
   hipStream_t keys_reader = nullptr;
+  uint64_t seq = 0;  // launch sequence number of the slot's last launch (frm_ctx::launch_seq)
+  // asynchronous readback (frm_read_frame_async / frm_present_async): the frame's bytes (or its
+  // blit) copied on the slot stream into a pinned host image; `copied` is recorded after the copy
+  uint8_t* host_img = nullptr;
+  size_t host_cap = 0;
+  uint8_t* present_dev = nullptr;  // frm_present_async's blit output (device), grown on demand
+  size_t present_dev_cap = 0;
+  hipEvent_t copied = nullptr;
+  uint64_t copy_ticket = 0;  // 0: no readback held
+  size_t copy_bytes = 0;
 };
 
 struct frm_ctx {
@@ -71,6 +81,11 @@ struct frm_ctx {
   uint32_t nslots = 1;
   uint32_t next_slot = 0;  // slot of the next launch
   uint32_t last_slot = 0;  // slot of the last frm_render (the frame read_frame/present see)
+  uint64_t launch_seq = 0;  // render launches so far (Slot::seq)
+  uint64_t render_seq = 0;  // launch_seq of the last frm_render
+  uint64_t ticket_seq = 0;  // asynchronous readbacks so far
+  frm_parameters render_params{};  // the parameters of the last frm_render (frm_debug_trace)
+  SceneUniforms render_scene{};
   ReloadedKernels* reloaded = nullptr;  // frm_reload: kernels compiled from edited sources
   uint8_t* present_buf = nullptr;  // frm_present output, grown on demand
   size_t present_cap = 0;
@@ -200,9 +215,32 @@ int synchronize_all(frm_ctx* ctx) {
 
 // The stream frm_render uses for slot i (created on first use: a context with one frame in
 // flight never creates more than the context stream).
+// Slots > 0 get a stream on a hardware queue of its own: HIP maps streams onto at most
+// GPU_MAX_HW_QUEUES queues per process (4 by default) and hands the least-used one out again,
+// and two frames whose streams share a queue never overlap. The runtime
+// never pools CU-masked queues, so a stream created with a mask of every CU (no restriction) has
+// its own queue whatever the host's queue limit and other streams; plain stream as a fallback.
+hipStream_t own_queue_stream(int device) {
+  hipDeviceProp_t prop;
+  const char* kind = getenv("FRM_SLOT_STREAMS");  // experiments: "plain" = pooled non-blocking stream
+  const bool plain = kind && strcmp(kind, "plain") == 0;
+  if (!plain && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
+    const uint32_t words = (uint32_t)(prop.multiProcessorCount + 31) / 32u;
+    uint32_t mask[64];
+    if (words <= 64u) {
+      for (uint32_t w = 0; w < words; ++w) mask[w] = 0xFFFFFFFFu;
+      hipStream_t s = nullptr;
+      if (hipExtStreamCreateWithCUMask(&s, words, mask) == hipSuccess) return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? s : nullptr;
+}
+
 int slot_stream(frm_ctx* ctx, uint32_t i, hipStream_t* out) {
   Slot& sl = ctx->slots[i];
-  if (!sl.stream) FRM_HIP(ctx, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+  if (!sl.stream && !(sl.stream = own_queue_stream(ctx->device)))
+    return fail(ctx, FRM_ERR_HIP, "stream creation failed for render slot %u", i);
   *out = sl.stream;
   return FRM_OK;
 }
@@ -311,6 +349,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   }
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded));
   FRM_HIP(ctx, hipEventRecord(sl.done, s));
+  sl.seq = ++ctx->launch_seq;
   sl.pending = true;
   sl.last_stream = s;
   ctx->next_slot = (si + 1u) % ctx->nslots;
@@ -384,6 +423,8 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
       if ((e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming)) != hipSuccess) rc = hip_fail(ctx, e, "hipEventCreate");
       else if ((e = hipEventCreateWithFlags(&sl.keys_read, hipEventDisableTiming)) != hipSuccess)
         rc = hip_fail(ctx, e, "hipEventCreate");
+      else if ((e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess)
+        rc = hip_fail(ctx, e, "hipEventCreate");
       else if ((e = hipMalloc(&sl.queue, 128)) != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc(queue)");
     }
   } while (0);
@@ -412,6 +453,9 @@ int frm_destroy(frm_ctx* ctx) {
       if (b) (void)hipFree(b);
     if (sl.done) (void)hipEventDestroy(sl.done);
     if (sl.keys_read) (void)hipEventDestroy(sl.keys_read);
+    if (sl.copied) (void)hipEventDestroy(sl.copied);
+    if (sl.host_img) (void)hipHostFree(sl.host_img);
+    if (sl.present_dev) (void)hipFree(sl.present_dev);
     if (i > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
   }
   if (ctx->present_buf) (void)hipFree(ctx->present_buf);
@@ -476,6 +520,9 @@ int frm_render(frm_ctx* ctx, frm_stats* stats) {
   rc = launch(ctx, a, s);
   if (rc) return rc;
   ctx->last_slot = si;
+  ctx->render_seq = sl.seq;
+  ctx->render_params = ctx->params;
+  ctx->render_scene = ctx->scene;
   if (stats) {
     FRM_HIP(ctx, hipEventRecord(ctx->ev_stop, s));
     uint64_t host[FRM_NUM_COUNTERS];
@@ -528,6 +575,75 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
   FRM_HIP(ctx, hipMemcpyAsync(dst, ctx->present_buf, need, hipMemcpyDeviceToHost, sl.stream));
   FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
   return FRM_OK;
+}
+
+// Enqueues the copy of `bytes` device bytes of the last frm_render's slot into its pinned host
+// image (on the slot stream, after the render) and hands out a ticket for it.
+static int readback_async(frm_ctx* ctx, Slot& sl, const uint8_t* src, size_t bytes, uint64_t* out_ticket) {
+  if (bytes > sl.host_cap) {
+    // the image's previous contents belong to an expired ticket (an earlier frame of this slot);
+    // only its copy may still be running
+    if (sl.copy_ticket) FRM_HIP(ctx, hipEventSynchronize(sl.copied));
+    if (sl.host_img) FRM_HIP(ctx, hipHostFree(sl.host_img));
+    sl.host_img = nullptr;
+    sl.host_cap = 0;
+    sl.copy_ticket = 0;
+    FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&sl.host_img), bytes, hipHostMallocDefault));
+    sl.host_cap = bytes;
+  }
+  FRM_HIP(ctx, hipMemcpyAsync(sl.host_img, src, bytes, hipMemcpyDeviceToHost, sl.stream));
+  FRM_HIP(ctx, hipEventRecord(sl.copied, sl.stream));
+  sl.copy_ticket = ++ctx->ticket_seq;
+  sl.copy_bytes = bytes;
+  *out_ticket = sl.copy_ticket;
+  return FRM_OK;
+}
+
+int frm_read_frame_async(frm_ctx* ctx, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/out_ticket is NULL");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->render_seq) return fail(ctx, FRM_ERR_NOT_READY, "no frm_render since the context was created");
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
+  return readback_async(ctx, sl, sl.fb, (size_t)ctx->width * ctx->height * 4u, out_ticket);
+}
+
+int frm_present_async(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags, uint64_t* out_ticket) {
+  if (!ctx || !out_ticket) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/out_ticket is NULL");
+  if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
+  if (!ctx->render_seq) return fail(ctx, FRM_ERR_NOT_READY, "no frm_render since the context was created");
+  if (out_width == 0 || out_height == 0 || out_width > FRM_MAX_DIMENSION || out_height > FRM_MAX_DIMENSION)
+    return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad output size %ux%u", out_width, out_height);
+  if (flags & ~(FRM_BLIT_SRGB | FRM_BLIT_BGRA)) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  Slot& sl = ctx->slots[ctx->last_slot];
+  const size_t need = (size_t)out_width * out_height * 4u;
+  if (need > sl.present_dev_cap) {  // its last use (an earlier frame of this slot) is stream-ordered before
+    FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
+    if (sl.present_dev) FRM_HIP(ctx, hipFree(sl.present_dev));
+    sl.present_dev = nullptr;
+    sl.present_dev_cap = 0;
+    FRM_HIP(ctx, hipMalloc(&sl.present_dev, need));
+    sl.present_dev_cap = need;
+  }
+  FRM_HIP(ctx, launch_blit(sl.fb, ctx->width, ctx->height, sl.present_dev, out_width, out_height, flags, sl.stream));
+  return readback_async(ctx, sl, sl.present_dev, need, out_ticket);
+}
+
+int frm_frame_pixels(frm_ctx* ctx, uint64_t ticket, const uint8_t** out_pixels, size_t* out_bytes) {
+  if (!ctx || !out_pixels) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/out_pixels is NULL");
+  for (uint32_t i = 0; i < ctx->nslots && ticket; ++i) {
+    Slot& sl = ctx->slots[i];
+    if (sl.copy_ticket != ticket) continue;
+    FRM_HIP(ctx, hipSetDevice(ctx->device));
+    FRM_HIP(ctx, hipEventSynchronize(sl.copied));
+    *out_pixels = sl.host_img;
+    if (out_bytes) *out_bytes = sl.copy_bytes;
+    return FRM_OK;
+  }
+  return fail(ctx, FRM_ERR_INVALID_ARGUMENT,
+              "ticket %llu is not held (expired: its slot has been read back again since, or never issued)",
+              (unsigned long long)ticket);
 }
 
 int frm_reload(frm_ctx* ctx, const char* source_dir) {
@@ -716,10 +832,19 @@ int frm_debug_trace(frm_ctx* ctx, float* out, size_t n_floats) {
   if (n_floats < npix * 10u)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "out holds %zu floats, the trace needs %zu", n_floats, npix * 10u);
   const Slot& sl = ctx->slots[ctx->last_slot];
+  if (!ctx->render_seq || sl.seq != ctx->render_seq)
+    return fail(ctx, FRM_ERR_NOT_READY, "no frm_render, or a later launch reused its slot's records");
   if (!sl.records || sl.records_cap < npix || !sl.sched_whole || sl.sched_w != ctx->width || sl.sched_h != ctx->height)
     return fail(ctx, FRM_ERR_NOT_READY, "the last frm_render was not a persistent launch of this frame size");
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  // the rays and colours of that render: its own parameters, not those set since
+  const frm_parameters cur_params = ctx->params;
+  const SceneUniforms cur_scene = ctx->scene;
+  ctx->params = ctx->render_params;
+  ctx->scene = ctx->render_scene;
   KernelArgs a = make_args(ctx, sl.fb, ctx->counters, ctx->height, 0, 1, ctx->height);
+  ctx->params = cur_params;
+  ctx->scene = cur_scene;
   a.geom = reinterpret_cast<ShadeGeom*>(sl.records);
   a.tails = reinterpret_cast<ShadeTail*>(sl.records + sl.records_cap * sizeof(ShadeGeom));
   float* d = nullptr;

@@ -118,6 +118,11 @@ SIGNATURES = [
     ("frm_reload", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     ("frm_present", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    ("frm_read_frame_async", ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_uint64)]),
+    ("frm_present_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint64)]),
+    ("frm_frame_pixels", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, _P(ctypes.POINTER(ctypes.c_uint8)), _P(ctypes.c_size_t)]),
     ("frm_band_rows_for", ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint32)]),
     ("frm_render_bands", ctypes.c_int,

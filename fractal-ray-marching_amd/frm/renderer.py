@@ -72,6 +72,31 @@ class Renderer:
         self._check(self._lib.frm_present(self.ctx, width, height, flags, buf.ctypes.data, buf.nbytes))
         return buf
 
+    # asynchronous readback (frm_read_frame_async / frm_present_async + frm_frame_pixels): the
+    # reference's surface presents with a frame of latency (wgpu's desired_maximum_frame_latency
+    # 2), so a loop renders frame k, starts its readback and then waits for frame k-1's pixels
+    def read_frame_async(self):
+        t = ctypes.c_uint64()
+        self._check(self._lib.frm_read_frame_async(self.ctx, ctypes.byref(t)))
+        return t.value
+
+    def present_async(self, width, height, srgb=True, bgra=False):
+        t = ctypes.c_uint64()
+        flags = (_lib.FRM_BLIT_SRGB if srgb else 0) | (_lib.FRM_BLIT_BGRA if bgra else 0)
+        self._check(self._lib.frm_present_async(self.ctx, width, height, flags, ctypes.byref(t)))
+        return t.value
+
+    def frame_pixels(self, ticket, shape=None, copy=True):
+        """Waits for the readback `ticket` and returns its pixels as a uint8 array of `shape`
+        (default: the frame's (height, width, 4)); copy=False returns a view of the library's
+        pinned image, valid until frames_in_flight further renders."""
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        self._check(self._lib.frm_frame_pixels(self.ctx, int(ticket), ctypes.byref(ptr), ctypes.byref(n)))
+        view = np.ctypeslib.as_array(ptr, shape=(n.value,))
+        view = view.reshape(shape or (self.height, self.width, 4))
+        return view.copy() if copy else view
+
     def synchronize(self):
         self._check(self._lib.frm_synchronize(self.ctx))
 

@@ -34,8 +34,10 @@
 extern "C" {
 #endif
 
-#define FRM_ABI_VERSION 3u  /* 2: frm_config.frames_in_flight (was reserved); 3: frm_render_bands_batch
-                               takes dst_bytes, frm_set_parameters bounds the fractal loop work */
+#define FRM_ABI_VERSION 4u  /* 2: frm_config.frames_in_flight (was reserved); 3: frm_render_bands_batch
+                               takes dst_bytes, frm_set_parameters bounds the fractal loop work;
+                               4: asynchronous readback (frm_read_frame_async, frm_present_async,
+                               frm_frame_pixels) */
 
 /* ---- status codes -------------------------------------------------------- */
 enum {
@@ -197,6 +199,28 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
                 size_t dst_bytes);
 int frm_synchronize(frm_ctx* ctx);
 
+/* ---- asynchronous readback: presentation with a frame of latency, as the reference's
+ *      surface has it. The reference configures its surface with wgpu's default
+ *      (persistent_graphics.rs:158-162, Surface::get_default_config:
+ *      desired_maximum_frame_latency = 2): present() and submit() return before the GPU has
+ *      drawn the frame, so the CPU prepares frame k+1 while frame k renders. With
+ *      frames_in_flight >= 2 the same loop on libfrm is
+ *          frm_render(k); frm_read_frame_async(&t[k]);      (both return at once)
+ *          frm_frame_pixels(t[k-1], &pixels);                (waits for frame k-1 only)
+ *      so frame k is already queued behind frame k-1 and fills the GPU while frame k-1's
+ *      longest pixels finish.
+ * frm_read_frame_async: enqueues the copy of the last frm_render's frame (frm_read_frame's
+ *      bytes) into a library-owned pinned host image of that frame's slot; returns a ticket.
+ * frm_present_async: the same for frm_present's blit output (out size, FRM_BLIT_* flags).
+ * frm_frame_pixels: waits for a ticket's copy and returns its pixels (4*w*h bytes, row 0 =
+ *      top). The image belongs to the render slot: it stays valid until frames_in_flight
+ *      further frm_render calls have been made (a later async readback of the same slot
+ *      replaces it); an expired or unknown ticket gives FRM_ERR_INVALID_ARGUMENT. */
+int frm_read_frame_async(frm_ctx* ctx, uint64_t* out_ticket);
+int frm_present_async(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t flags,
+                      uint64_t* out_ticket);
+int frm_frame_pixels(frm_ctx* ctx, uint64_t ticket, const uint8_t** out_pixels, size_t* out_bytes);
+
 /* The kernel (FRM_KERNEL_*) a render or band launch of `pixels` pixels runs on this
  * context: the FRM_FLAG_*_KERNEL flag when set, otherwise FRM_KERNEL_SIMPLE when pixels
  * is below one resident persistent grid (1536 lanes per CU) and FRM_KERNEL_PERSISTENT
@@ -285,7 +309,8 @@ int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n);
 int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n);
 
 /* frm_debug_trace: the geometric inputs of the shading of every pixel of the last frm_render (a
- * whole frame on the persistent kernel, the context's current size and parameters), 10 floats per
+ * whole frame on the persistent kernel, with the size and parameters that render used; refused
+ * with FRM_ERR_NOT_READY when a later launch has reused its slot), 10 floats per
  * pixel, row-major, in the layout of the oracle's per-pixel trace: hit, primary steps, normal xyz,
  * sun hit, sun closeness, object colour xyz (hits; zeros for misses). Parity tooling for frames
  * that are not bit-exact by design (FRM_FLAG_HW_MATH). n_floats >= 10 x width x height. */

@@ -31,7 +31,7 @@ def test_every_declared_symbol_is_exported(frm_lib):
 
 
 def test_abi_version(frm_lib):
-    assert frm_lib.frm_abi_version() == 3
+    assert frm_lib.frm_abi_version() == 4
 
 
 def test_struct_layout_matches_c(tmp_path):

@@ -137,7 +137,7 @@ def test_batch_rank_without_bands(frm_lib):
     counters = torch.zeros(8, dtype=torch.int64, device="cuda")
     with frm.Renderer(device=0, max_steps=64) as r:
         r.resize(w, h)
-        for stride in (0, 4):
-            r.render_bands_batch([a] * 3, buf.data_ptr(), 0, stride, br, 1, ranks, 0, counters.data_ptr())
+        for stride, nbytes in ((0, 0), (4, buf.numel())):
+            r.render_bands_batch([a] * 3, buf.data_ptr(), nbytes, stride, br, 1, ranks, 0, counters.data_ptr())
         torch.cuda.synchronize()
         assert int(counters.sum()) == 0 and int(buf.sum()) == 0

@@ -1,13 +1,25 @@
 #!/bin/bash
-# Build an alternative libfrm (extra compile flags) into fractal-ray-marching_amd/variants/NAME.so
-# without touching lib/libfrm.so. Usage: bash tools/build_variant.sh NAME "-DFOO=1 ..."
+# Build an alternative libfrm for an A/B into fractal-ray-marching_amd/ab/NAME.so without touching
+# lib/libfrm.so: extra compile flags and/or a patch applied to a copy of csrc/ (experiments live as
+# patches under profiles/, never in the product sources). Delete ab/ after the A/B: every gpurun
+# call ships it.
+# Usage: PATCH=profiles/round4/ab_prio/prio.patch bash tools/build_variant.sh NAME "-DFOO=1 ..."
 # (SCHEDFLAGS=... in the environment replaces the Makefile's scheduler options, e.g. SCHEDFLAGS="")
 set -e
 NAME=$1; FLAGS=$2
-cd "$(dirname "$0")/../fractal-ray-marching_amd"
-mkdir -p variants
-make -s OBJDIR=build/obj_$NAME EXTRA_HIPFLAGS="$FLAGS" ${SCHEDFLAGS+SCHEDFLAGS="$SCHEDFLAGS"} build/obj_$NAME/frm_kernels.o build/obj_$NAME/frm_api.o \
-  build/obj_$NAME/frm_sched.o build/obj_$NAME/frm_host.o build/obj_$NAME/frm_reload.o
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o variants/$NAME.so build/obj_$NAME/frm_kernels.o \
-  build/obj_$NAME/frm_api.o build/obj_$NAME/frm_sched.o build/obj_$NAME/frm_host.o build/obj_$NAME/frm_reload.o -lhiprtc
-echo "variants/$NAME.so"
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+cd "$ROOT/fractal-ray-marching_amd"
+SRC=csrc
+if [ -n "$PATCH" ]; then
+  SRC=build/src_$NAME
+  rm -rf "$SRC"; mkdir -p "$SRC"
+  cp csrc/* "$SRC/"
+  (cd "$SRC" && patch -s -p3 < "$ROOT/$PATCH")
+fi
+OBJ=build/obj_$NAME
+mkdir -p ab
+make -s CSRC="$SRC" OBJDIR=$OBJ EXTRA_HIPFLAGS="$FLAGS" ${SCHEDFLAGS+SCHEDFLAGS="$SCHEDFLAGS"} $OBJ/frm_kernels.o $OBJ/frm_api.o \
+  $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ab/$NAME.so $OBJ/frm_kernels.o \
+  $OBJ/frm_api.o $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o -lhiprtc
+echo "ab/$NAME.so"

@@ -54,6 +54,7 @@ def frames_per_dispatch(d):
 
 def main(d):
     c = {}
+    c3 = load(d, "sq3")  # where the wave cycles go (SQ_WAVE_CYCLES of that pass)
     for n in ("sq", "sq2", "wr", "rd"):
         c.update(load(d, n))
     trace = glob.glob(f"{d}/sq/**/*kernel_trace.csv", recursive=True)
@@ -76,6 +77,20 @@ def main(d):
         "salu_insts": c.get("SQ_INSTS_SALU"),
         "waves": c["SQ_WAVES"],
         "wait_inst_any_frac": c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"],
+        "active_inst_any_frac": c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"],
+        "smem_insts": c.get("SQ_INSTS_SMEM"),
+        "vmem_insts": c.get("SQ_INSTS_VMEM"),
+        # pass sq3 (its own SQ_WAVE_CYCLES): wave-parked (s_waitcnt / barrier) cycles, scalar /
+        # misc / LDS issue, SALU and SMEM instruction cycles, branches (quad-cycle units cancel)
+        "sq3": ({
+            "wait_any_frac": c3["SQ_WAIT_ANY"] / c3["SQ_WAVE_CYCLES"],
+            "active_inst_sca_frac": c3["SQ_ACTIVE_INST_SCA"] / c3["SQ_WAVE_CYCLES"],
+            "active_inst_misc_frac": c3["SQ_ACTIVE_INST_MISC"] / c3["SQ_WAVE_CYCLES"],
+            "active_inst_lds_frac": c3["SQ_ACTIVE_INST_LDS"] / c3["SQ_WAVE_CYCLES"],
+            "inst_cycles_salu_frac": c3["SQ_INST_CYCLES_SALU"] / c3["SQ_WAVE_CYCLES"],
+            "inst_cycles_smem_frac": c3["SQ_INST_CYCLES_SMEM"] / c3["SQ_WAVE_CYCLES"],
+            "branch_insts": c3["SQ_INSTS_BRANCH"],
+        } if c3 else None),
         "hbm_write_bytes": c.get("WRITE_SIZE", 0) * 1024,
         "hbm_read_bytes": 2 * c.get("FETCH_SIZE", 0) * 1024,
         "hbm_write_gbps": c.get("WRITE_SIZE", 0) * 1024 / t / 1e9,
