@@ -61,8 +61,12 @@ struct KernelArgs {
   FrameCamera cams[kMaxBatch];
 };
 
+// One wave per workgroup: a persistent wave frees its CU slot the moment its last pixel ends, not
+// when the slowest of a 4-wave workgroup's does, so the next frame in flight fills the slots of a
+// draining frame sooner (round 4, profiles/round4/ab_wg: moving-camera drop-in loop 12.62 -> 12.33
+// ms/frame, HEADLINE_FLY 11.96 -> 11.75; headline, C2, C3 and the 8-way share unchanged)
 #ifndef FRM_MARCH_BLOCK
-#define FRM_MARCH_BLOCK 256
+#define FRM_MARCH_BLOCK 64
 #endif
 constexpr uint32_t kMarchBlock = FRM_MARCH_BLOCK;  // march_persistent threads per workgroup
 constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
