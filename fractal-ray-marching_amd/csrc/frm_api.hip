@@ -339,12 +339,13 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
     sl.sched_whole = whole;
     sl.sched_w = a.f.width;
     sl.sched_h = a.f.height;
-    a.debug = (unsigned long long*)(sl.queue + 8);  // bytes 32..71 of the queue block
-    FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, sizeof(unsigned int), s));
+    unsigned int* dbg = sl.queue + kQueueDebugWord;
+    a.debug = (unsigned long long*)dbg;  // the diagnostic words after the partition counters
+    FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, kQueueDebugWord * sizeof(unsigned int), s));
 #ifdef FRM_STAMPS
-    FRM_HIP(ctx, hipMemsetAsync(sl.queue + 8, 0, 16, s));
-    FRM_HIP(ctx, hipMemsetAsync(sl.queue + 12, 0xff, 16, s));  // atomicMin slots
-    FRM_HIP(ctx, hipMemsetAsync(sl.queue + 16, 0, 8, s));
+    FRM_HIP(ctx, hipMemsetAsync(dbg, 0, 16, s));
+    FRM_HIP(ctx, hipMemsetAsync(dbg + 4, 0xff, 16, s));  // atomicMin slots
+    FRM_HIP(ctx, hipMemsetAsync(dbg + 8, 0, 8, s));
 #endif
   }
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded));
@@ -425,7 +426,7 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
         rc = hip_fail(ctx, e, "hipEventCreate");
       else if ((e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess)
         rc = hip_fail(ctx, e, "hipEventCreate");
-      else if ((e = hipMalloc(&sl.queue, 128)) != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc(queue)");
+      else if ((e = hipMalloc(&sl.queue, kQueueBytes)) != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc(queue)");
     }
   } while (0);
   if (rc != FRM_OK) {
@@ -789,7 +790,7 @@ int frm_unshuffle_bands(frm_ctx* ctx, const uint8_t* dev_src, size_t rank_stride
 #ifdef FRM_STAMPS
 extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
   const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
-  return hipMemcpy(out5, sl.queue + 8, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+  return hipMemcpy(out5, sl.queue + kQueueDebugWord, 40, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 #endif
 

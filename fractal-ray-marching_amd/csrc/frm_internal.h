@@ -69,6 +69,22 @@ struct KernelArgs {
 #define FRM_MARCH_BLOCK 64
 #endif
 constexpr uint32_t kMarchBlock = FRM_MARCH_BLOCK;  // march_persistent threads per workgroup
+// The persistent kernel's work queue (its chunks of 64 fetch positions, most expensive first),
+// XCD-aware. One claim counter for the whole GPU serialised every claim at one address: C3 waves
+// parked 57 % of their cycles in the claim's wait (PMC SQ_WAIT_ANY; tools/diag_waves.py: the refill
+// block took 62 % of wave time). Now the head of the order (its first 1/kQueueHeadDiv chunks, the
+// most expensive) is claimed from one shared counter, so waves of every XCD start the frame's
+// longest pixels first; the rest is dealt round-robin over kQueueParts partitions (chunk c to
+// partition c % kQueueParts, keeping the order's slope in each), one per XCD, each claimed through
+// its own counter in its own 256-B line by the waves of that XCD (HW_REG_XCC_ID); a wave whose
+// partition is drained moves on to the next. C3 1.75 -> 1.11 ms, the others within noise
+// (profiles/round4/ab_xq). Placement only ever changes which lane computes a pixel, never its bytes.
+constexpr uint32_t kQueueParts = 8;         // MI355X: 8 XCDs
+constexpr uint32_t kQueueHeadDiv = 8;       // the shared head: nchunks / 8 chunks (1/4: C3 +5 %)
+constexpr uint32_t kQueuePartWords = 64;    // u32 words between two counters (256 B); the head's is
+                                            // counter kQueueParts
+constexpr uint32_t kQueueDebugWord = (kQueueParts + 1u) * kQueuePartWords;  // FRM_STAMPS words after the counters
+constexpr size_t kQueueBytes = (kQueueDebugWord + 64u) * 4u;
 constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
 
 #if !defined(__HIPCC_RTC__)  // host-side launchers; hiprtc only needs the types above

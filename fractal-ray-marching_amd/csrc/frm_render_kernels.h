@@ -78,6 +78,9 @@ constexpr uint32_t kChunk = 64u;  // pixels per queue fetch (one per lane of the
 enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// The XCD (XCC) this wave runs on, 0..7 on MI355X (s_getreg HW_REG_XCC_ID): its work-queue
+// partition (frm_internal.h kQueueParts). Placement only, never a pixel's bytes.
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kQueueParts - 1u); }
 __device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(ballot(c)); }
 
 // Scheduling key of a finished pixel: 16 x log2(cost + 1), 0..255 (~4.4 % steps); cost =
@@ -121,6 +124,11 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   // wave-uniform state: current chunk of 64 fetched pixels, how many were handed out
   uint32_t slots_used = kChunk;
   bool exhausted = false;
+  // the work-queue partition the wave claims from (its XCD's first, kQueueParts in frm_internal.h)
+  // and the partitions it has found drained
+  const uint32_t nchunks = (total + kChunk - 1u) / kChunk;
+  uint32_t part = xcc_id(), drained = 0;
+  const uint32_t nhead = nchunks / kQueueHeadDiv;
   uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
 #ifdef FRM_COUNT_EXACT
   uint64_t n_dbg_total = 0, n_dbg_exact = 0;
@@ -277,13 +285,39 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     const uint64_t want = ballot(pix == kIdle);
     if (want != 0 && !exhausted) {
       if (slots_used == kChunk) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.queue, kChunk);
-        base = uniform(__shfl(base, 0, 64));
+        // claim the next chunk of the wave's partition; chunk j of partition x is queue chunk
+        // j * kQueueParts + x. A drained partition passes the wave on to the next one.
+        uint32_t base = kIdle;
+        // the head of the order (its most expensive chunks) from the shared counter
+        if (!(drained >> kQueueParts)) {
+          uint32_t j = 0;
+          if (lane == 0) j = atomicAdd(a.queue + kQueueParts * kQueuePartWords, 1u);
+          j = uniform(__shfl(j, 0, 64));
+          if (j < nhead)
+            base = j * kChunk;
+          else
+            drained |= 1u << kQueueParts;
+        }
+        // then chunk j of the XCD's partition x is queue chunk nhead + j * kQueueParts + x; a
+        // drained partition passes the wave on to the next one
+        while (base == kIdle) {
+          uint32_t j = 0;
+          if (lane == 0) j = atomicAdd(a.queue + part * kQueuePartWords, 1u);
+          j = uniform(__shfl(j, 0, 64));
+          const uint32_t c = nhead + j * kQueueParts + part;
+          if (c < nchunks) {
+            base = c * kChunk;
+            break;
+          }
+          drained |= 1u << part;
+          if ((drained & ((1u << kQueueParts) - 1u)) == (1u << kQueueParts) - 1u) break;
+          do part = (part + 1u) % kQueueParts;
+          while ((drained >> part) & 1u);
+        }
 #ifdef FRM_STAMPS
         n_fetch++;
 #endif
-        if (base >= total) {
+        if (base == kIdle) {
           exhausted = true;
 #ifdef FRM_STAMPS
           real_exhaust = __builtin_amdgcn_s_memrealtime();

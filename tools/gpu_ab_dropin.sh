@@ -9,13 +9,15 @@ for round in $(seq 1 ${ROUNDS:-2}); do
   for n in $VARIANTS; do
     export FRM_LIB=$PWD/fractal-ray-marching_amd/ab/$n.so
     timeout -k 10 200 python tools/dropin_probe.py --workload HEADLINE_FLY --forms latency,latency3 > "$OUT/dropin_${n}_$round.jsonl" 2> "$OUT/dropin_${n}_$round.err" || { echo "dropin $n failed"; tail -5 "$OUT/dropin_${n}_$round.err"; exit 1; }
+    timeout -k 10 200 python tools/dropin_probe.py --workload HEADLINE --forms latency > "$OUT/dropinfix_${n}_$round.jsonl" 2> "$OUT/dropinfix_${n}_$round.err" || { echo "dropin fixed $n failed"; tail -5 "$OUT/dropinfix_${n}_$round.err"; exit 1; }
     timeout -k 10 200 python bench.py --workload HEADLINE_FLY --no-cpu-baseline --no-dropin > "$OUT/fly_${n}_$round.json" 2> "$OUT/fly_${n}_$round.err" || { echo "fly $n failed"; tail -5 "$OUT/fly_${n}_$round.err"; exit 1; }
     python - "$OUT" "$n" "$round" <<'PY'
 import json, sys
 out, n, r = sys.argv[1:]
 d = [json.loads(l) for l in open(f"{out}/dropin_{n}_{r}.jsonl")]
 f = json.load(open(f"{out}/fly_{n}_{r}.json"))
-print(f"round {r} {n}: dropin " + " ".join(f"{x['form']} {x['ms_per_frame']:.3f}" for x in d) + f" | fly bench {f['ms_per_step']:.3f} ms sha_ok {f['frame_sha_ok']}")
+x = json.loads(open(f"{out}/dropinfix_{n}_{r}.jsonl").read().splitlines()[-1])
+print(f"round {r} {n}: dropin fly " + " ".join(f"{x['form']} {x['ms_per_frame']:.3f}" for x in d) + f" | fixed {x['ms_per_frame']:.3f} | fly bench {f['ms_per_step']:.3f} ms sha_ok {f['frame_sha_ok']}")
 PY
   done
 done

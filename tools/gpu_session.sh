@@ -30,15 +30,20 @@ configs)
   done
   echo CONFIGS_OK ;;
 pmc)
-  for spec in "HEADLINE:--steps 4 --warmup 2" "C2:--steps 4 --warmup 2" "C3:--steps 4 --warmup 2" "C4:--steps 2 --warmup 1" "C5:--steps 2 --warmup 1"; do
+  # PMC_SPECS: "WORKLOAD:bench args" entries separated by '|' (default: every config); SHARE8=1 adds
+  # one rank's share of the 8-way split
+  IFS='|' read -r -a specs <<< "${PMC_SPECS:-HEADLINE:--steps 4 --warmup 2|C2:--steps 4 --warmup 2|C3:--steps 4 --warmup 2|C4:--steps 2 --warmup 1|C5:--steps 2 --warmup 1}"
+  for spec in "${specs[@]}"; do
     wl=${spec%%:*}; a=${spec#*:}
     OUT="$OUT/pmc_raw/$wl" ARGS="--workload $wl $a --no-cpu-baseline --no-dropin" bash tools/pmc.sh > /dev/null || { echo "pmc $wl failed"; exit 1; }
     python tools/pmc_summary.py "$OUT/pmc_raw/$wl" > "$OUT/pmc_${wl}_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/$wl" shade_pass > "$OUT/pmc_${wl}_shade.json" || exit 1
-    python -c "import json;s=json.load(open('$OUT/pmc_${wl}_march.json'));print('$wl', 'valu_busy', round(s['valu_busy'],3), 'lane_util', round(s['valu_lane_utilization'],3), 'valu_insts/frame %.3g' % (s['valu_wave_insts']/s['frames_per_dispatch']))"
+    python -c "import json;s=json.load(open('$OUT/pmc_${wl}_march.json'));print('$wl', 'valu_busy', round(s['valu_busy'],3), 'lane_util', round(s['valu_lane_utilization'],3), 'valu_insts/frame %.3g' % (s['valu_wave_insts']/s['frames_per_dispatch']), 'sq3', s.get('sq3'))"
   done
-  # one rank's share of bench.py's 8-way row split (rank 0, 2 launches in flight, 10 frames per launch)
-  OUT="$OUT/pmc_raw/HEADLINE_share8" PROG=tools/pipeline_probe.py ARGS="--workloads HEADLINE --ranks 8 --inflight 2 --batch 10 --frames 40" bash tools/pmc.sh > /dev/null || { echo "pmc share8 failed"; exit 1; }
-  python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" > "$OUT/pmc_HEADLINE_share8_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" shade_pass > "$OUT/pmc_HEADLINE_share8_shade.json" || exit 1
+  if [ -n "$SHARE8" ]; then
+    # one rank's share of bench.py's 8-way row split (rank 0, 2 launches in flight, 10 frames per launch)
+    OUT="$OUT/pmc_raw/HEADLINE_share8" PROG=tools/pipeline_probe.py ARGS="--workloads HEADLINE --ranks 8 --inflight 2 --batch 10 --frames 40" bash tools/pmc.sh > /dev/null || { echo "pmc share8 failed"; exit 1; }
+    python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" > "$OUT/pmc_HEADLINE_share8_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" shade_pass > "$OUT/pmc_HEADLINE_share8_shade.json" || exit 1
+  fi
   echo PMC_OK ;;
 *) echo "PART=tests|configs|pmc"; exit 2 ;;
 esac
