@@ -77,10 +77,20 @@ constexpr uint32_t kMarchBlock = FRM_MARCH_BLOCK;  // march_persistent threads p
 // longest pixels first; the rest is dealt round-robin over kQueueParts partitions (chunk c to
 // partition c % kQueueParts, keeping the order's slope in each), one per XCD, each claimed through
 // its own counter in its own 256-B line by the waves of that XCD (HW_REG_XCC_ID); a wave whose
-// partition is drained moves on to the next. C3 1.75 -> 1.11 ms, the others within noise
-// (profiles/round4/ab_xq). Placement only ever changes which lane computes a pixel, never its bytes.
-constexpr uint32_t kQueueParts = 8;         // MI355X: 8 XCDs
-constexpr uint32_t kQueueHeadDiv = 8;       // the shared head: nchunks / 8 chunks (1/4: C3 +5 %)
+// partition is drained moves on to the next. C3 1.75 -> 1.11 ms, headline 10.40 -> 10.25 ms, the
+// moving-camera loops within noise (profiles/round4/ab_xq; 32 partitions or a head of 1/32: no
+// better, profiles/round4/ab_qs). Placement only ever changes which lane computes a pixel, never
+// its bytes.
+#ifndef FRM_QUEUE_PARTS
+#define FRM_QUEUE_PARTS 8
+#endif
+#ifndef FRM_QUEUE_HEAD_DIV
+#define FRM_QUEUE_HEAD_DIV 8
+#endif
+constexpr uint32_t kXcds = 8;                           // MI355X
+constexpr uint32_t kQueueParts = FRM_QUEUE_PARTS;       // a multiple of kXcds: kQueueParts / 8 per XCD
+constexpr uint32_t kQueueHeadDiv = FRM_QUEUE_HEAD_DIV;  // the shared head: nchunks / kQueueHeadDiv chunks
+static_assert(kQueueParts % kXcds == 0 && kQueueParts <= 32, "queue partitions: a multiple of the XCDs, <= 32");
 constexpr uint32_t kQueuePartWords = 64;    // u32 words between two counters (256 B); the head's is
                                             // counter kQueueParts
 constexpr uint32_t kQueueDebugWord = (kQueueParts + 1u) * kQueuePartWords;  // FRM_STAMPS words after the counters

@@ -78,9 +78,14 @@ constexpr uint32_t kChunk = 64u;  // pixels per queue fetch (one per lane of the
 enum Phase : uint32_t { kPrimary = 0, kTap0 = 1, kTap3 = 4, kShadow = 5 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-// The XCD (XCC) this wave runs on, 0..7 on MI355X (s_getreg HW_REG_XCC_ID): its work-queue
-// partition (frm_internal.h kQueueParts). Placement only, never a pixel's bytes.
-__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kQueueParts - 1u); }
+// The work-queue partition a wave claims from first (frm_internal.h kQueueParts): one of the
+// kQueueParts / 8 partitions of the XCD (XCC) it runs on (s_getreg HW_REG_XCC_ID, 0..7), picked by
+// its workgroup index (workgroups b and b + 8 share an XCD). Placement only, never a pixel's bytes.
+__device__ __forceinline__ uint32_t queue_part() {
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1u);
+  constexpr uint32_t per = kQueueParts / kXcds;
+  return xcc * per + (per > 1u ? (blockIdx.x / kXcds) % per : 0u);
+}
 __device__ __forceinline__ uint64_t count(bool c) { return (uint64_t)__popcll(ballot(c)); }
 
 // Scheduling key of a finished pixel: 16 x log2(cost + 1), 0..255 (~4.4 % steps); cost =
@@ -127,7 +132,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   // the work-queue partition the wave claims from (its XCD's first, kQueueParts in frm_internal.h)
   // and the partitions it has found drained
   const uint32_t nchunks = (total + kChunk - 1u) / kChunk;
-  uint32_t part = xcc_id(), drained = 0;
+  uint32_t part = queue_part();
+  uint64_t drained = 0;  // bit x: partition x drained; bit kQueueParts: the head
   const uint32_t nhead = nchunks / kQueueHeadDiv;
   uint64_t n_pix = 0, n_hit = 0, n_prim = 0, n_shadow = 0, n_body = 0, n_bail = 0;
 #ifdef FRM_COUNT_EXACT
@@ -285,8 +291,6 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     const uint64_t want = ballot(pix == kIdle);
     if (want != 0 && !exhausted) {
       if (slots_used == kChunk) {
-        // claim the next chunk of the wave's partition; chunk j of partition x is queue chunk
-        // j * kQueueParts + x. A drained partition passes the wave on to the next one.
         uint32_t base = kIdle;
         // the head of the order (its most expensive chunks) from the shared counter
         if (!(drained >> kQueueParts)) {
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           if (j < nhead)
             base = j * kChunk;
           else
-            drained |= 1u << kQueueParts;
+            drained |= 1ull << kQueueParts;
         }
         // then chunk j of the XCD's partition x is queue chunk nhead + j * kQueueParts + x; a
         // drained partition passes the wave on to the next one
@@ -309,8 +313,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
             base = c * kChunk;
             break;
           }
-          drained |= 1u << part;
-          if ((drained & ((1u << kQueueParts) - 1u)) == (1u << kQueueParts) - 1u) break;
+          drained |= 1ull << part;
+          if ((drained & ((1ull << kQueueParts) - 1ull)) == (1ull << kQueueParts) - 1ull) break;
           do part = (part + 1u) % kQueueParts;
           while ((drained >> part) & 1u);
         }

@@ -53,7 +53,7 @@ print(f"service pass cycles: consume {cons.sum() / nserv.sum():.0f}, refill {ref
       f"start-DE+counters {(scyc.sum() - cons.sum() - refl.sum()) / nserv.sum():.0f}; "
       f"fetches per wave {nfetch.mean():.1f}")
 sub = [rec[:, 11 + k].astype(np.float64).sum() / nserv.sum() for k in range(4)]
-print("consume sub-blocks, cycles per pass: distance %.0f, primary %.0f, taps %.0f, shadow %.0f" % tuple(sub))
+print("sub-stamps, cycles per pass: [0] %.0f, [1] %.0f, [2] %.0f, [3] %.0f" % tuple(sub))
 print(f"wave start spread {st.max():.0f} us; first exhaust {np.nanmin(ex):.0f} us, median exhaust {np.nanmedian(ex):.0f} us")
 q = np.percentile(en, [0, 10, 50, 90, 99, 100])
 print("wave end percentiles (us): " + " ".join(f"p{p_}={v:.0f}" for p_, v in zip([0, 10, 50, 90, 99, 100], q)))
