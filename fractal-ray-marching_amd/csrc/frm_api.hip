@@ -38,7 +38,15 @@ struct Slot {
   hipEvent_t done = nullptr;     // recorded after the slot's last launch (any stream)
   bool pending = false;          // `done` has been recorded since the slot was last waited for
   hipStream_t last_stream = nullptr;  // stream of the slot's last launch
-  uint8_t* fb = nullptr;         // frm_render's framebuffer for this slot
+  // frm_render's framebuffers for this slot (context pool), used alternately: a frame's
+  // asynchronous readback (copy stream) overlaps the slot's next render, which writes the other
+  // one; fb is the current one. Capacity: a smaller frame size keeps the larger buffer.
+  uint8_t* fbs[2] = {nullptr, nullptr};
+  size_t fbs_cap[2] = {0, 0};
+  hipEvent_t fb_read[2] = {nullptr, nullptr};  // after the last asynchronous readback of fbs[i]
+  bool fb_read_pending[2] = {false, false};
+  uint32_t fb_idx = 0;
+  uint8_t* fb = nullptr;
   unsigned int* queue = nullptr;
   uint8_t* records = nullptr;  // persistent kernel scratch (ShadeGeom[cap] then ShadeTail[cap]), grown on demand
   size_t records_cap = 0;
@@ -58,11 +66,21 @@ struct Slot {
   hipEvent_t keys_read = nullptr;
   hipStream_t keys_reader = nullptr;
   uint64_t seq = 0;  // launch sequence number of the slot's last launch (frm_ctx::launch_seq)
+  // fused scheduling (KernelArgs::key_hist): two launches' histogram + cursor words, used
+  // alternately; order_ready: the slot's last launch ranked its pixels into sched_order and zeroed
+  // the queue and the other half of rank_words for geometry order_key
+  uint32_t* rank_words = nullptr;
+  uint32_t rank_half = 0;
+  bool order_ready = false;
+  uint64_t order_key = 0;
   // asynchronous readback (frm_read_frame_async / frm_present_async): the frame's bytes (or its
-  // blit) copied on the slot stream into a pinned host image; `copied` is recorded after the copy
+  // blit) copied into a pinned host image on the slot's copy stream, after the render (`done`);
+  // `copied` is recorded after the copy, and the slot's next frm_render waits for it before its
+  // launch rewrites the framebuffer. The render stream itself goes straight on to the next frame.
+  hipStream_t copy_stream = nullptr;
   uint8_t* host_img = nullptr;
   size_t host_cap = 0;
-  uint8_t* present_dev = nullptr;  // frm_present_async's blit output (device), grown on demand
+  uint8_t* present_dev = nullptr;  // frm_present_async's blit output (device, context pool), grown on demand
   size_t present_dev_cap = 0;
   hipEvent_t copied = nullptr;
   uint64_t copy_ticket = 0;  // 0: no readback held
@@ -75,6 +93,11 @@ struct frm_ctx {
   uint32_t flags = 0;
   int cu_count = 0;
   hipStream_t stream = nullptr;  // the context stream (= slots[0].stream)
+  // Stream-ordered pool of the buffers that follow the frame size (framebuffers, persistent-kernel
+  // records, scheduling arrays, presentation output): they are released and re-allocated on the
+  // stream that uses them, so frm_resize never drains the frames in flight. Freed blocks stay in
+  // the pool (release threshold: never) for the next size change.
+  hipMemPool_t pool = nullptr;
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   uint32_t width = 0, height = 0;
   Slot slots[FRM_MAX_FRAMES_IN_FLIGHT];
@@ -91,6 +114,7 @@ struct frm_ctx {
   size_t present_cap = 0;
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   uint32_t service_min = kDefaultServiceMin;
+  bool fused_sched = true;  // KernelArgs::key_hist; FRM_SCHED=sort: every launch sorts (experiments)
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
@@ -122,6 +146,43 @@ int hip_fail(frm_ctx* ctx, hipError_t e, const char* what) {
     hipError_t e_ = (call);                             \
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
   } while (0)
+
+// Device memory of the context pool, allocated / released in the order of stream s: a block
+// released on s is reused only by work ordered after everything enqueued on s before the release.
+int dev_alloc(frm_ctx* ctx, void** p, size_t bytes, hipStream_t s) {
+  FRM_HIP(ctx, hipMallocFromPoolAsync(p, bytes, ctx->pool, s));
+  return FRM_OK;
+}
+int dev_release(frm_ctx* ctx, void* p, hipStream_t s) {
+  if (p) FRM_HIP(ctx, hipFreeAsync(p, s));
+  return FRM_OK;
+}
+// Slot sl's framebuffer for a frame of `bytes`, grown on the slot stream (renders and synchronous
+// readback use it there; an asynchronous readback on the copy stream is awaited first).
+int ensure_fb(frm_ctx* ctx, Slot& sl, size_t bytes) {
+  const uint32_t i = sl.fb_idx;
+  sl.fb = sl.fbs[i];
+  if (sl.fbs_cap[i] >= bytes) return FRM_OK;
+  int rc = dev_release(ctx, sl.fbs[i], sl.stream);  // after its readback: frm_render / frm_resize wait
+  if (rc) return rc;
+  sl.fbs[i] = sl.fb = nullptr;
+  sl.fbs_cap[i] = 0;
+  if ((rc = dev_alloc(ctx, (void**)&sl.fbs[i], bytes, sl.stream))) return rc;
+  sl.fbs_cap[i] = bytes;
+  sl.fb = sl.fbs[i];
+  return FRM_OK;
+}
+// Makes fbs[i] the slot's current framebuffer, its last asynchronous readback ordered before
+// everything enqueued on the slot stream from here on.
+int select_fb(frm_ctx* ctx, Slot& sl, uint32_t i) {
+  sl.fb_idx = i;
+  sl.fb = sl.fbs[i];
+  if (sl.fb_read_pending[i]) {
+    FRM_HIP(ctx, hipStreamWaitEvent(sl.stream, sl.fb_read[i], 0));
+    sl.fb_read_pending[i] = false;
+  }
+  return FRM_OK;
+}
 
 uint32_t num_bands(uint32_t height, uint32_t band_rows) { return (height + band_rows - 1) / band_rows; }
 
@@ -185,6 +246,8 @@ KernelArgs make_args(frm_ctx* ctx, uint8_t* dst, unsigned long long* counters, u
   a.batch = 1;
   a.rec_stride = local_rows * ctx->width;
   a.out_stride = local_rows * ctx->width;
+  memcpy(a.cams[0].row, a.f.row, sizeof(a.f.row));  // a single frame is a batch of one
+  a.cams[0].origin = a.f.origin;
   return a;
 }
 
@@ -262,12 +325,12 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   if (kind == kKernelPersistent) {
     const size_t need = (size_t)a.g.local_rows * a.f.width * a.batch;
     if (need > sl.records_cap) {  // grows outside the steady state (first frame of a size)
-      int rc = wait_slot(ctx, sl);
+      // stream-ordered: s runs after the slot's last launch (awaited above when on another stream)
+      int rc = dev_release(ctx, sl.records, s);
       if (rc) return rc;
-      if (sl.records) FRM_HIP(ctx, hipFree(sl.records));
       sl.records = nullptr;
       sl.records_cap = 0;
-      FRM_HIP(ctx, hipMalloc(&sl.records, need * kRecordBytes));
+      if ((rc = dev_alloc(ctx, (void**)&sl.records, need * kRecordBytes, s))) return rc;
       sl.records_cap = need;
     }
     a.geom = reinterpret_cast<ShadeGeom*>(sl.records);
@@ -291,27 +354,27 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
         if (j != si && o.sched_history && o.sched_key == key && o.sched_cap >= npix) donor = (int)j;
       }
     if (npix > sl.sched_cap) {
-      int rc = wait_slot(ctx, sl);
-      if (rc) return rc;
+      // stream-ordered like the records; a donor's copy of these keys was awaited above
       uint8_t* old_keys = sl.sched_keys;  // kept until a resize has resampled it
+      int rc = FRM_OK;
       for (void* b : {(void*)sl.sched_iota, (void*)sl.sched_order, sl.sched_temp})
-        if (b) FRM_HIP(ctx, hipFree(b));
-      if (!rescale && old_keys) FRM_HIP(ctx, hipFree(old_keys));
+        if ((rc = dev_release(ctx, b, s))) return rc;
+      if (!rescale && (rc = dev_release(ctx, old_keys, s))) return rc;
       sl.sched_iota = sl.sched_order = nullptr;
       sl.sched_keys = nullptr;
       sl.sched_temp = nullptr;
       sl.sched_cap = 0;
       sl.sched_temp_bytes = schedule_temp_bytes(npix);
-      FRM_HIP(ctx, hipMalloc(&sl.sched_iota, (size_t)npix * sizeof(uint32_t)));
-      FRM_HIP(ctx, hipMalloc(&sl.sched_order, (size_t)npix * sizeof(uint32_t)));
-      FRM_HIP(ctx, hipMalloc(&sl.sched_keys, (size_t)npix * 2));
-      FRM_HIP(ctx, hipMalloc(&sl.sched_temp, sl.sched_temp_bytes ? sl.sched_temp_bytes : 16));
+      if ((rc = dev_alloc(ctx, (void**)&sl.sched_iota, (size_t)npix * sizeof(uint32_t), s)) ||
+          (rc = dev_alloc(ctx, (void**)&sl.sched_order, (size_t)npix * sizeof(uint32_t), s)) ||
+          (rc = dev_alloc(ctx, (void**)&sl.sched_keys, (size_t)npix * 2, s)) ||
+          (rc = dev_alloc(ctx, &sl.sched_temp, sl.sched_temp_bytes ? sl.sched_temp_bytes : 16, s)))
+        return rc;
       FRM_HIP(ctx, fill_iota(sl.sched_iota, npix, s));
       sl.sched_cap = npix;
       if (rescale) {
         FRM_HIP(ctx, rescale_keys(old_keys, sl.sched_w, sl.sched_h, sl.sched_keys, a.f.width, a.f.height, s));
-        FRM_HIP(ctx, hipStreamSynchronize(s));  // the old map is read before it is freed
-        FRM_HIP(ctx, hipFree(old_keys));
+        if ((rc = dev_release(ctx, old_keys, s))) return rc;  // after the resample reads it
       }
     } else if (rescale) {
       // resample into the sort's output half, then back (the map is read and written)
@@ -329,9 +392,24 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
       FRM_HIP(ctx, hipEventRecord(dn.keys_read, s));  // the donor's next launch waits for this copy
       dn.keys_reader = s;
     }
-    const bool history = same || rescale || donor >= 0;
-    FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
-                                 sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
+    // the steady state: the slot's last launch (same geometry) has already ranked its pixels and
+    // reset this launch's counters in its shading pass, so nothing runs between the two launches
+    const bool fused = same && sl.order_ready && sl.order_key == key;
+    uint32_t* half = sl.rank_words + sl.rank_half * kRankWords;
+    if (!fused) {
+      const bool history = same || rescale || donor >= 0;
+      FRM_HIP(ctx, schedule_pixels(npix, history, sl.sched_keys, sl.sched_keys + sl.sched_cap,
+                                   sl.sched_iota, sl.sched_order, sl.sched_temp, sl.sched_temp_bytes, s));
+      FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, kQueueDebugWord * sizeof(unsigned int), s));
+      FRM_HIP(ctx, hipMemsetAsync(half, 0, kRankWords * sizeof(uint32_t), s));
+    }
+    // runtime-reloaded kernels may not rank (edited sources): the next launch sorts again
+    const bool rank = ctx->reloaded == nullptr && ctx->fused_sched;
+    a.key_hist = rank ? half : nullptr;
+    a.key_hist_next = sl.rank_words + (sl.rank_half ^ 1u) * kRankWords;
+    a.order_out = sl.sched_order;
+    sl.order_ready = false;  // set below once the launch is enqueued
+    sl.order_key = key;
     a.pixel_order = sl.sched_order;
     a.pixel_key = sl.sched_keys;
     sl.sched_key = key;
@@ -341,14 +419,18 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
     sl.sched_h = a.f.height;
     unsigned int* dbg = sl.queue + kQueueDebugWord;
     a.debug = (unsigned long long*)dbg;  // the diagnostic words after the partition counters
-    FRM_HIP(ctx, hipMemsetAsync(sl.queue, 0, kQueueDebugWord * sizeof(unsigned int), s));
 #ifdef FRM_STAMPS
     FRM_HIP(ctx, hipMemsetAsync(dbg, 0, 16, s));
     FRM_HIP(ctx, hipMemsetAsync(dbg + 4, 0xff, 16, s));  // atomicMin slots
     FRM_HIP(ctx, hipMemsetAsync(dbg + 8, 0, 8, s));
 #endif
   }
+  if (kind != kKernelPersistent) sl.order_ready = false;
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded));
+  if (a.key_hist) {
+    sl.order_ready = true;
+    sl.rank_half ^= 1u;
+  }
   FRM_HIP(ctx, hipEventRecord(sl.done, s));
   sl.seq = ++ctx->launch_seq;
   sl.pending = true;
@@ -404,6 +486,7 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   ctx->max_steps = config->max_steps ? config->max_steps : FRM_DEFAULT_MAX_STEPS;
   ctx->flags = config->flags;
   ctx->nslots = config->frames_in_flight ? config->frames_in_flight : 1u;
+  if (const char* env = getenv("FRM_SCHED")) ctx->fused_sched = strcmp(env, "sort") != 0;
   if (const char* env = getenv("FRM_SERVICE_MIN")) {
     long v = strtol(env, nullptr, 10);
     if (v >= 1 && v <= 64) ctx->service_min = (uint32_t)v;
@@ -415,6 +498,17 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
       rc = hip_fail(ctx, e, "hipDeviceGetAttribute"); break;
     }
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) { rc = hip_fail(ctx, e, "hipStreamCreate"); break; }
+    hipMemPoolProps props;
+    memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = ctx->device;
+    if ((e = hipMemPoolCreate(&ctx->pool, &props)) != hipSuccess) { rc = hip_fail(ctx, e, "hipMemPoolCreate"); break; }
+    uint64_t keep = UINT64_MAX;
+    if ((e = hipMemPoolSetAttribute(ctx->pool, hipMemPoolAttrReleaseThreshold, &keep)) != hipSuccess) {
+      rc = hip_fail(ctx, e, "hipMemPoolSetAttribute"); break;
+    }
     if ((e = hipEventCreate(&ctx->ev_start)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
     if ((e = hipEventCreate(&ctx->ev_stop)) != hipSuccess) { rc = hip_fail(ctx, e, "hipEventCreate"); break; }
     if ((e = hipMalloc(&ctx->counters, FRM_NUM_COUNTERS * sizeof(unsigned long long))) != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc(counters)"); break; }
@@ -426,7 +520,12 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
         rc = hip_fail(ctx, e, "hipEventCreate");
       else if ((e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess)
         rc = hip_fail(ctx, e, "hipEventCreate");
+      else if ((e = hipEventCreateWithFlags(&sl.fb_read[0], hipEventDisableTiming)) != hipSuccess ||
+               (e = hipEventCreateWithFlags(&sl.fb_read[1], hipEventDisableTiming)) != hipSuccess)
+        rc = hip_fail(ctx, e, "hipEventCreate");
       else if ((e = hipMalloc(&sl.queue, kQueueBytes)) != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc(queue)");
+      else if ((e = hipMalloc(&sl.rank_words, 2 * kRankWords * sizeof(uint32_t))) != hipSuccess)
+        rc = hip_fail(ctx, e, "hipMalloc(rank words)");
     }
   } while (0);
   if (rc != FRM_OK) {
@@ -445,20 +544,29 @@ int frm_destroy(frm_ctx* ctx) {
   for (uint32_t i = 0; i < ctx->nslots; ++i) {
     Slot& sl = ctx->slots[i];
     if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+    if (sl.copy_stream) (void)hipStreamSynchronize(sl.copy_stream);
     if (sl.pending) (void)hipEventSynchronize(sl.done);
   }
   for (uint32_t i = 0; i < ctx->nslots; ++i) {
     Slot& sl = ctx->slots[i];
-    for (void* b : {(void*)sl.fb, (void*)sl.queue, (void*)sl.records, (void*)sl.sched_iota, (void*)sl.sched_order,
-                    (void*)sl.sched_keys, sl.sched_temp})
-      if (b) (void)hipFree(b);
+    // pool blocks back to the pool (every stream is idle), then the pool itself below
+    if (ctx->stream)
+      for (void* b : {(void*)sl.fbs[0], (void*)sl.fbs[1], (void*)sl.records, (void*)sl.sched_iota, (void*)sl.sched_order,
+                      (void*)sl.sched_keys, sl.sched_temp, (void*)sl.present_dev})
+        if (b) (void)hipFreeAsync(b, ctx->stream);
+    if (sl.queue) (void)hipFree(sl.queue);
+    if (sl.rank_words) (void)hipFree(sl.rank_words);
     if (sl.done) (void)hipEventDestroy(sl.done);
     if (sl.keys_read) (void)hipEventDestroy(sl.keys_read);
     if (sl.copied) (void)hipEventDestroy(sl.copied);
+    for (hipEvent_t ev : sl.fb_read)
+      if (ev) (void)hipEventDestroy(ev);
     if (sl.host_img) (void)hipHostFree(sl.host_img);
-    if (sl.present_dev) (void)hipFree(sl.present_dev);
     if (i > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
+    if (sl.copy_stream) (void)hipStreamDestroy(sl.copy_stream);
   }
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
   if (ctx->present_buf) (void)hipFree(ctx->present_buf);
   unload_reloaded(ctx->reloaded);
   if (ctx->counters) (void)hipFree(ctx->counters);
@@ -476,15 +584,14 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
                 FRM_MAX_DIMENSION);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->slots[0].fb && width == ctx->width && height == ctx->height) return FRM_OK;
-  int rc = synchronize_all(ctx);
-  if (rc) return rc;
-  for (uint32_t i = 0; i < ctx->nslots; ++i) {  // slots > 0 allocate theirs at first use
-    Slot& sl = ctx->slots[i];
-    if (sl.fb) FRM_HIP(ctx, hipFree(sl.fb));
-    sl.fb = nullptr;
-  }
-  ctx->width = ctx->height = 0;
-  FRM_HIP(ctx, hipMalloc(&ctx->slots[0].fb, (size_t)width * height * 4u));
+  if (!ctx->slots[0].stream) return fail(ctx, FRM_ERR_HIP, "context stream missing");
+  // No drain: frames in flight finish at their own size. Every buffer that follows the size grows
+  // in its stream's order when a launch of the new size needs it (ensure_fb, launch); slot 0's
+  // framebuffer (what frm_read_frame sees before the next frm_render) grows here.
+  const size_t bytes = (size_t)width * height * 4u;
+  Slot& s0 = ctx->slots[0];
+  int rc = select_fb(ctx, s0, s0.fb_idx);
+  if (rc || (rc = ensure_fb(ctx, s0, bytes + bytes / 4u))) return rc;  // headroom for the reference's +-1 steps
   ctx->width = width;
   ctx->height = height;
   ctx->last_slot = 0;
@@ -512,7 +619,11 @@ int frm_render(frm_ctx* ctx, frm_stats* stats) {
   Slot& sl = ctx->slots[si];
   hipStream_t s;
   if ((rc = slot_stream(ctx, si, &s))) return rc;
-  if (!sl.fb) FRM_HIP(ctx, hipMalloc(&sl.fb, (size_t)ctx->width * ctx->height * 4u));
+  // the other framebuffer of the slot: the last one may still be read back (copy stream); this
+  // one's readback (two renders of the slot ago) is awaited on the slot stream, long done
+  if ((rc = select_fb(ctx, sl, sl.fb_idx ^ 1u))) return rc;
+  const size_t fb_bytes = (size_t)ctx->width * ctx->height * 4u;
+  if ((rc = ensure_fb(ctx, sl, fb_bytes + fb_bytes / 4u))) return rc;
   KernelArgs a = make_args(ctx, sl.fb, ctx->counters, ctx->height, 0, 1, ctx->height);
   if (stats) {
     FRM_HIP(ctx, hipMemsetAsync(ctx->counters, 0, FRM_NUM_COUNTERS * sizeof(unsigned long long), s));
@@ -578,8 +689,15 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
   return FRM_OK;
 }
 
+// The slot's copy stream, ordered after the slot's last launch (its render).
+static int copy_stream_after_render(frm_ctx* ctx, Slot& sl) {
+  if (!sl.copy_stream) FRM_HIP(ctx, hipStreamCreateWithFlags(&sl.copy_stream, hipStreamNonBlocking));
+  FRM_HIP(ctx, hipStreamWaitEvent(sl.copy_stream, sl.done, 0));
+  return FRM_OK;
+}
+
 // Enqueues the copy of `bytes` device bytes of the last frm_render's slot into its pinned host
-// image (on the slot stream, after the render) and hands out a ticket for it.
+// image (on the slot's copy stream, after copy_stream_after_render) and hands out a ticket for it.
 static int readback_async(frm_ctx* ctx, Slot& sl, const uint8_t* src, size_t bytes, uint64_t* out_ticket) {
   if (bytes > sl.host_cap) {
     // the image's previous contents belong to an expired ticket (an earlier frame of this slot);
@@ -589,11 +707,16 @@ static int readback_async(frm_ctx* ctx, Slot& sl, const uint8_t* src, size_t byt
     sl.host_img = nullptr;
     sl.host_cap = 0;
     sl.copy_ticket = 0;
-    FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&sl.host_img), bytes, hipHostMallocDefault));
-    sl.host_cap = bytes;
+    // headroom: a +-1 step of the reference's render-texture factor (4 % per axis) reuses it
+    const size_t cap = bytes + bytes / 4u;
+    FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&sl.host_img), cap, hipHostMallocDefault));
+    sl.host_cap = cap;
   }
-  FRM_HIP(ctx, hipMemcpyAsync(sl.host_img, src, bytes, hipMemcpyDeviceToHost, sl.stream));
-  FRM_HIP(ctx, hipEventRecord(sl.copied, sl.stream));
+  FRM_HIP(ctx, hipMemcpyAsync(sl.host_img, src, bytes, hipMemcpyDeviceToHost, sl.copy_stream));
+  FRM_HIP(ctx, hipEventRecord(sl.copied, sl.copy_stream));
+  // the framebuffer is read (by this copy, or by frm_present_async's blit before it) until here
+  FRM_HIP(ctx, hipEventRecord(sl.fb_read[sl.fb_idx], sl.copy_stream));
+  sl.fb_read_pending[sl.fb_idx] = true;
   sl.copy_ticket = ++ctx->ticket_seq;
   sl.copy_bytes = bytes;
   *out_ticket = sl.copy_ticket;
@@ -606,6 +729,8 @@ int frm_read_frame_async(frm_ctx* ctx, uint64_t* out_ticket) {
   if (!ctx->render_seq) return fail(ctx, FRM_ERR_NOT_READY, "no frm_render since the context was created");
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
+  int rc = copy_stream_after_render(ctx, sl);
+  if (rc) return rc;
   return readback_async(ctx, sl, sl.fb, (size_t)ctx->width * ctx->height * 4u, out_ticket);
 }
 
@@ -619,15 +744,17 @@ int frm_present_async(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uin
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   Slot& sl = ctx->slots[ctx->last_slot];
   const size_t need = (size_t)out_width * out_height * 4u;
-  if (need > sl.present_dev_cap) {  // its last use (an earlier frame of this slot) is stream-ordered before
-    FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
-    if (sl.present_dev) FRM_HIP(ctx, hipFree(sl.present_dev));
+  int rc = copy_stream_after_render(ctx, sl);
+  if (rc) return rc;
+  if (need > sl.present_dev_cap) {  // its last use (an earlier frame of this slot) is ordered before, on the copy stream
+    if ((rc = dev_release(ctx, sl.present_dev, sl.copy_stream))) return rc;
     sl.present_dev = nullptr;
     sl.present_dev_cap = 0;
-    FRM_HIP(ctx, hipMalloc(&sl.present_dev, need));
+    if ((rc = dev_alloc(ctx, (void**)&sl.present_dev, need, sl.copy_stream))) return rc;
     sl.present_dev_cap = need;
   }
-  FRM_HIP(ctx, launch_blit(sl.fb, ctx->width, ctx->height, sl.present_dev, out_width, out_height, flags, sl.stream));
+  FRM_HIP(ctx, launch_blit(sl.fb, ctx->width, ctx->height, sl.present_dev, out_width, out_height, flags,
+                           sl.copy_stream));
   return readback_async(ctx, sl, sl.present_dev, need, out_ticket);
 }
 
@@ -751,6 +878,8 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
     // modules carry the single-frame kernels only)
     for (uint32_t k = 0; k < count; ++k) {
       compute_frame_uniforms(params[k], ctx->width, ctx->height, ctx->max_steps, &a.f);
+      memcpy(a.cams[0].row, a.f.row, sizeof(a.f.row));
+      a.cams[0].origin = a.f.origin;
       a.out = (uint32_t*)(dev_dst + (size_t)k * frame_stride_bytes);
       int rc = launch(ctx, a, s);
       if (rc) return rc;
@@ -820,6 +949,7 @@ int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
   if (rc) return rc;
   if (sl.keys_reader) FRM_HIP(ctx, hipEventSynchronize(sl.keys_read));
   FRM_HIP(ctx, hipMemcpy(sl.sched_keys, keys, n, hipMemcpyHostToDevice));
+  sl.order_ready = false;  // the next launch sorts by these keys
   return FRM_OK;
 }
 

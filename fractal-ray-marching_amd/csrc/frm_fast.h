@@ -107,14 +107,9 @@ __device__ __forceinline__ uint32_t xor_sign_(uint32_t v, uint32_t m) {
 #endif
 }
 __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
-#ifdef FRM_FAST_V1
-  float j = rintf(x * kTwoOverPi);
-  const uint32_t q = (uint32_t)(int)j;
-#else
   const float tq = x * kTwoOverPi + 0x1.8p23f;
   const float j = tq - 0x1.8p23f;
   const uint32_t q = __float_as_uint(tq);
-#endif
   float r = fma_(-j, kHalfPi, x);
   r = fma_(-j, kHalfPiLo, r);
   float z = r * r;
@@ -123,15 +118,9 @@ __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out
   float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
                   4.166664568298827e-2f);
   float c = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
-#ifdef FRM_FAST_V1
-  const bool odd = (q & 1u) != 0u;
-  float sv = odd ? c : s;
-  float cv = odd ? s : c;
-#else
   const uint32_t odd = (uint32_t)((int32_t)(q << 31) >> 31);  // v_bfe_i32 q, 0, 1
   const float sv = __uint_as_float(bfi_(odd, __float_as_uint(c), __float_as_uint(s)));
   const float cv = __uint_as_float(bfi_(odd, __float_as_uint(s), __float_as_uint(c)));
-#endif
   *s_out = __uint_as_float(xor_sign_(__float_as_uint(sv), q << 30));
   *c_out = __uint_as_float(xor_sign_(__float_as_uint(cv), (q + 1u) << 30));
 }
@@ -147,7 +136,6 @@ __device__ __forceinline__ float acos_dev(float t) {
   float p = fma_(fma_(fma_(fma_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
                       7.4953002686e-2f), z, 1.6666752422e-1f);
   float s = fma_(w * z, p, w);
-#ifndef FRM_ACOS_SELECT
   // rb is used only for |t| > 1/2 (t != 0): t > 0 is t's sign bit, and (t > 0 ? 2s : pi - 2s)
   // == fma(2s, t < 0 ? -1 : 1, t < 0 ? pi : 0), one rounding either way
   const uint32_t tb = __float_as_uint(t);
@@ -155,9 +143,6 @@ __device__ __forceinline__ float acos_dev(float t) {
   // the offset (t < 0 ? pi : 0) as fma(sg, -pi/2, pi/2): exact (+0 or pi), one FMA-class
   // instruction instead of a shift and a mask
   float rb = fma_(2.0f * s, sg, fma_(sg, -0.5f * kPi, 0.5f * kPi));
-#else
-  float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
-#endif
   // pi/2 - copysign(s, t) == fma(-sg, s, pi/2): sg * s is exact (+-s; t = -0 gives sg = -1)
   float rs = fma_(-sg, s, kHalfPi);
   return big ? rb : rs;
@@ -181,7 +166,6 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
                           0.10678940285181907f), s, -0.14214209135918496f), s,
                 0.1999413720560495f), s, -0.3333316696611865f);
   float r = fma_(a * s, q, a);
-#ifndef FRM_ATAN_SELECT
   // the octant fix-ups without compares: (c ? h - r : r) == fma(r, c ? -1 : 1, c ? h : 0), one
   // rounding either way (r >= +0); the +-1 is a bit-field insert of c's sign bit into 1.0.
   // c = sign bit of ax - ay (exact difference: negative iff ay > ax, +0 when equal) and of
@@ -192,10 +176,6 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
   // offsets (c ? h : 0) as fma(s, -h/2, h/2): exact (+0 or h)
   r = fma_(r, s1, fma_(s1, -0.5f * kHalfPi, 0.5f * kHalfPi));
   r = fma_(r, s2, fma_(s2, -0.5f * kPi, 0.5f * kPi));
-#else
-  r = (ay > ax) ? kHalfPi - r : r;
-  r = (x < 0.0f) ? kPi - r : r;
-#endif
   return copysignf(r, y);
 }
 
@@ -205,13 +185,9 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
 // as frexp + the doubling below sqrt(1/2) (x = m0 * 2^e, m0 in [1/2, 1): m0 >= sqrt(1/2)
 // keeps m0, else 2 m0 with e - 1), without v_frexp, the compare and the selects.
 __device__ __forceinline__ void log_split_normal(float x, float* f_out, float* e_out) {
-#ifdef FRM_FAST_V1
-  log_split_(x, f_out, e_out);
-#else
   const uint32_t ix = __float_as_uint(x) - 0x3f3504f3u;  // bits of kSqrtHalf
   *f_out = __uint_as_float(__float_as_uint(x) - (ix & 0xff800000u)) - 1.0f;
   *e_out = (float)((int32_t)ix >> 23);
-#endif
 }
 
 // log2_ for positive normal finite x.
@@ -236,21 +212,13 @@ __device__ __forceinline__ float log_posnormal(float x) {
 // (one v_lshl_add_u32 in place of v_rndne, v_cvt and v_ldexp). The clamp to [-151, 129]
 // cannot fire there.
 __device__ __forceinline__ float exp2_tame(float y) {
-#ifdef FRM_FAST_V1
-  float k = rintf(y);
-#else
   const float t = y + 0x1.8p23f;
   const float k = t - 0x1.8p23f;
-#endif
   float f = y - k;
   float p = fma_(fma_(fma_(fma_(fma_(1.535336188319500e-4f, f, 1.339887440266574e-3f), f,
                                9.618437357674640e-3f), f, 5.550332471162809e-2f), f,
                      2.402264791363012e-1f), f, 6.931472028550421e-1f);
-#ifdef FRM_FAST_V1
-  return ldexpf(fma_(f, p, 1.0f), (int)k);
-#else
   return __uint_as_float(__float_as_uint(fma_(f, p, 1.0f)) + (__float_as_uint(t) << 23));
-#endif
 }
 
 #endif  // __HIP_DEVICE_COMPILE__

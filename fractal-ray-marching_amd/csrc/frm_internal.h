@@ -54,12 +54,26 @@ struct KernelArgs {
   // work queue; queue chunk c (64 positions) holds pixel_order[(c / batch) * 64 + 0..63] of
   // frame c % batch (each frame's pixels heaviest first, frames interleaved chunk by chunk).
   // Frame k's records start at k * rec_stride, its output at out + k * out_stride, its
-  // camera is cams[k]. batch = 1: f.row / f.origin.
+  // camera is cams[k]. batch = 1: cams[0] = f.row / f.origin (the built-in persistent kernel
+  // reads cams[] for every launch; frm_reload's single-frame kernels read f).
   uint32_t batch;
   uint32_t rec_stride;            // records per frame
   uint32_t out_stride;            // packed RGBA8 words per frame
+  // Fused scheduling (frm_api.hip launch; nullptr: off). The shading pass counts the cost keys
+  // of the launch's last frame into key_hist[0..255]; rank_pass then ranks the local pixels by
+  // descending key into order_out (the 8-bit counting sort the hipcub path does: bucket bases from
+  // that histogram, per-block ranges reserved through the cursors key_hist[256..511]), the fetch
+  // order of the slot's next launch; the shading pass also zeroes that launch's histogram and
+  // cursors (key_hist_next[0..511]) and its work-queue counters. A steady-state frame then has two
+  // short dispatches (shade, rank) between its march and the slot's next march, instead of the
+  // queue memset and the hipcub sort's dispatches.
+  uint32_t* key_hist;
+  uint32_t* key_hist_next;
+  uint32_t* order_out;
   FrameCamera cams[kMaxBatch];
 };
+constexpr uint32_t kRankWords = 512;  // one launch's key_hist: 256 counts + 256 cursors
+constexpr uint32_t kShadeBlockPixels = 4096;  // shade_pass / rank_pass: local pixels per 256-thread block
 
 // One wave per workgroup: a persistent wave frees its CU slot the moment its last pixel ends, not
 // when the slowest of a 4-wave workgroup's does, so the next frame in flight fills the slots of a

@@ -158,13 +158,17 @@ static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStre
   return hipModuleLaunchKernel(fn, grid.x, grid.y, grid.z, block.x, block.y, block.z, 0, stream, params, nullptr);
 }
 
+// Every built-in persistent launch, a single frame included, runs the multi-frame instantiation
+// (a single frame is a batch of one, its camera in cams[0]): the single-frame one needs 82 VGPRs
+// on ROCm 7.2 (5 waves/SIMD), the multi-frame one 80 (6 waves/SIMD).
 template <uint32_t FAM, bool ITERS>
 static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStream_t stream,
                                     const ReloadedKernels* rk) {
   static int blocks_per_cu = 0;  // occupancy of this instantiation (per process)
   if (blocks_per_cu == 0) {
     int n = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS>, kMarchBlock, 0);
+    hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS, true>, kMarchBlock, 0);
     if (e != hipSuccess) return e;
     blocks_per_cu = n > 0 ? n : 1;
   }
@@ -177,16 +181,17 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) blocks = 1;
   const uint32_t pixels = args.g.local_rows * args.f.width;
+  const uint32_t shade_blocks = (pixels + kShadeBlockPixels - 1u) / kShadeBlockPixels;
   if (rk) {
     hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(kMarchBlock), stream, args);
     if (e != hipSuccess) return e;
-    return module_launch(rk->shade[FAM], dim3((pixels + 255u) / 256u, args.batch), dim3(256), stream, args);
+    return module_launch(rk->shade[FAM], dim3(shade_blocks, args.batch), dim3(256), stream, args);
   }
-  if (args.batch > 1)
-    hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
-  else
-    hipLaunchKernelGGL((march_persistent<FAM, ITERS>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
-  hipLaunchKernelGGL((shade_pass<FAM>), dim3((pixels + 255u) / 256u, args.batch), dim3(256), 0, stream, args);
+  hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+  hipLaunchKernelGGL((shade_pass<FAM>), dim3(shade_blocks, args.batch), dim3(256), 0, stream, args);
+  if (args.key_hist)  // fused scheduling: the slot's next fetch order
+    hipLaunchKernelGGL(rank_pass, dim3((args.npix + kShadeBlockPixels - 1u) / kShadeBlockPixels), dim3(256), 0, stream,
+                       args.pixel_key, args.npix, args.key_hist, args.order_out);
   return hipGetLastError();
 }
 

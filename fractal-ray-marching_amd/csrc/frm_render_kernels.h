@@ -278,8 +278,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     if (fin) {  // primary miss (flags 0: BACKGROUND_COLOR) or end of the shadow march
       FRM_SUB_BEGIN();
       const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
-      *reinterpret_cast<uint2*>(&tails[pix]) =
-          make_uint2(__float_as_uint(closeness), psteps | flags | ((uint32_t)cost_key(pix_cost) << kRecKeyShift));
+      const uint32_t ck = cost_key(pix_cost);
+      *reinterpret_cast<uint2*>(&tails[pix]) = make_uint2(__float_as_uint(closeness), psteps | flags | (ck << kRecKeyShift));
       pix = kIdle;
       FRM_SUB_END(3);
     }
@@ -452,24 +452,26 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   }
 }
 
-// Coherent shading of the records written by march_persistent: fragment.wgsl:333-348
-// (+ the Rgba8UnormSrgb store). One thread per local pixel, row-major.
-template <uint32_t FAM>
-__global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
-  __shared__ float table[256];
-  table[threadIdx.x] = kSrgbThresholds[threadIdx.x];
+// Exclusive prefix sum over the 256 threads of a block (4 waves), one value per thread.
+__device__ __forceinline__ uint32_t block_exclusive_scan256(uint32_t v, uint32_t* wave_tot) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(inc, off, 64);
+    if (lane >= (uint32_t)off) inc += u;
+  }
+  if (lane == 63u) wave_tot[wave] = inc;
   __syncthreads();
-  const uint32_t width = a.f.width;
-  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
-  if (idx >= a.g.local_rows * width) return;
-  const uint32_t lr = idx / width, x = idx - lr * width;
-  const uint32_t y = band_row_to_global(a.g, lr);
-  if (y >= a.f.height) return;
-  const uint32_t fr = blockIdx.y;  // frame of a multi-frame launch (0 otherwise)
-  const uint32_t rec = fr * a.rec_stride + idx;
-  const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[rec]);
-  // coalesced, for the next launch's order (a multi-frame launch: its last frame's costs)
-  if (a.pixel_key && fr + 1u == a.batch) a.pixel_key[idx] = (uint8_t)(r1.y >> kRecKeyShift);
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < wave; ++w) before += wave_tot[w];
+  return before + inc - v;
+}
+
+// The shading of one pixel's records (fragment.wgsl:333-348 + the Rgba8UnormSrgb store).
+template <uint32_t FAM>
+__device__ __forceinline__ void shade_record(const KernelArgs& a, uint2 r1, uint32_t rec, uint32_t fr, uint32_t idx,
+                                             uint32_t x, uint32_t y, const float* table) {
   uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
   if (r1.y & kRecHit) {
     const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[rec]);
@@ -483,6 +485,80 @@ __global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
     word = pack_rgba(color, table);
   }
   a.out[(size_t)fr * a.out_stride + idx] = word;
+}
+
+// Coherent shading of the records written by march_persistent: fragment.wgsl:333-348
+// (+ the Rgba8UnormSrgb store). A block shades kShadeBlockPixels local pixels, row-major, 256
+// at a time (coalesced). With fused scheduling (KernelArgs::key_hist) it also counts the cost
+// keys of the launch's last frame (an LDS histogram per block, one global add per key present:
+// few blocks, so few adds on the hot keys' counters) and resets the slot's next launch.
+template <uint32_t FAM>
+__global__ __launch_bounds__(256) void shade_pass(KernelArgs a) {
+  __shared__ float table[256];
+  __shared__ uint32_t s_count[256];
+  const uint32_t t = threadIdx.x;
+  const uint32_t fr = blockIdx.y;  // frame of a multi-frame launch (0 otherwise)
+  // fused scheduling: the key histogram of the launch's last frame (block-uniform)
+  const bool hist = a.key_hist != nullptr && fr + 1u == a.batch;
+  table[t] = kSrgbThresholds[t];
+  if (hist) s_count[t] = 0u;
+  __syncthreads();
+  const uint32_t width = a.f.width, local = a.g.local_rows * width;
+  for (uint32_t j = 0; j < kShadeBlockPixels / 256u; ++j) {
+    const uint32_t idx = (blockIdx.x * (kShadeBlockPixels / 256u) + j) * 256u + t;
+    if (idx >= local) break;
+    const uint32_t lr = idx / width, x = idx - lr * width;
+    const uint32_t y = band_row_to_global(a.g, lr);
+    if (y >= a.f.height) break;  // the short last band's missing rows: the launch's last local rows
+    const uint32_t rec = fr * a.rec_stride + idx;
+    const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[rec]);
+    const uint32_t key = r1.y >> kRecKeyShift;
+    // coalesced, for the next launch's order (a multi-frame launch: its last frame's costs)
+    if (a.pixel_key && fr + 1u == a.batch) a.pixel_key[idx] = (uint8_t)key;
+    if (hist) atomicAdd(&s_count[key], 1u);
+    shade_record<FAM>(a, r1, rec, fr, idx, x, y, table);
+  }
+  if (!hist) return;
+  __syncthreads();
+  if (const uint32_t c = s_count[t]) atomicAdd(a.key_hist + t, c);
+  if (blockIdx.x == 0) {  // the slot's next launch starts from zeroed counts, cursors and queue
+    a.key_hist_next[t] = 0u;
+    a.key_hist_next[256u + t] = 0u;
+    for (uint32_t w = t; w < kQueueDebugWord; w += 256u) a.queue[w] = 0u;
+  }
+}
+
+// Fused scheduling, after shade_pass: the next launch's fetch order, the local pixels by descending
+// cost key (an 8-bit counting sort: bucket bases from the shading pass's histogram, one range per
+// block and bucket reserved through the cursors key_hist[256..511], the block's kShadeBlockPixels
+// pixels ranked in LDS). Ties are ordered by block, then as the LDS atomics happen to run: the
+// order places pixels on lanes, it never changes a pixel's bytes.
+__global__ __launch_bounds__(256) void rank_pass(const uint8_t* __restrict__ keys, uint32_t npix,
+                                                 uint32_t* __restrict__ hist, uint32_t* __restrict__ order) {
+  constexpr uint32_t kPer = kShadeBlockPixels / 256u;
+  __shared__ uint32_t s_base[256], s_count[256], s_res[256], s_wave[4];
+  const uint32_t t = threadIdx.x;
+  s_count[t] = 0u;
+  __syncthreads();
+  uint32_t key[kPer], rank[kPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    const uint32_t idx = (blockIdx.x * kPer + j) * 256u + t;
+    key[j] = idx < npix ? keys[idx] : 0u;
+    rank[j] = idx < npix ? atomicAdd(&s_count[key[j]], 1u) : 0u;
+  }
+  // bucket bases in descending key order: base[k] = pixels with a key above k
+  const uint32_t k_desc = 255u - t;
+  s_base[k_desc] = block_exclusive_scan256(hist[k_desc], s_wave);  // its barrier completes s_count
+  const uint32_t c = s_count[t];
+  s_res[t] = c ? atomicAdd(hist + 256u + t, c) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    const uint32_t idx = (blockIdx.x * kPer + j) * 256u + t;
+    const uint32_t pos = s_base[key[j]] + s_res[key[j]] + rank[j];
+    if (idx < npix && pos < npix) order[pos] = idx;  // pos < npix always, for a histogram of these keys
+  }
 }
 
 // dst row y <- band b = y / band_rows, held by rank b % ranks as its (b / ranks)-th band.

@@ -324,11 +324,7 @@ __device__ __forceinline__ uint32_t comp_key(float v) { return (__float_as_uint(
 __device__ __forceinline__ bool mb_tame(v3 z, float r) {
   constexpr uint32_t kMin = (0x21800000u << 1) - 1u;  // comp_key(0x1p-60f)
   const uint32_t m = min(min(comp_key(z.x), comp_key(z.y)), comp_key(z.z));  // v_min3_u32
-#ifdef FRM_FAST_V1
-  return (r >= 0x1p-40f) & (m >= kMin);
-#else
   return (r >= 0x1p-13f) & (m >= kMin);
-#endif
 }
 
 // mb_body (frm_scene.h) with the tame primitives: the same operations in the same order.

@@ -78,13 +78,21 @@ class Renderer:
     def read_frame_async(self):
         t = ctypes.c_uint64()
         self._check(self._lib.frm_read_frame_async(self.ctx, ctypes.byref(t)))
-        return t.value
+        return self._remember(t.value, (self.height, self.width, 4))
 
     def present_async(self, width, height, srgb=True, bgra=False):
         t = ctypes.c_uint64()
         flags = (_lib.FRM_BLIT_SRGB if srgb else 0) | (_lib.FRM_BLIT_BGRA if bgra else 0)
         self._check(self._lib.frm_present_async(self.ctx, width, height, flags, ctypes.byref(t)))
-        return t.value
+        return self._remember(t.value, (height, width, 4))
+
+    def _remember(self, ticket, shape):
+        # a ticket keeps the shape of its frame across a later resize (frm_resize does not drain)
+        shapes = self.__dict__.setdefault("_ticket_shapes", {})
+        shapes[ticket] = shape
+        if len(shapes) > 64:
+            del shapes[min(shapes)]
+        return ticket
 
     def frame_pixels(self, ticket, shape=None, copy=True):
         """Waits for the readback `ticket` and returns its pixels as a uint8 array of `shape`
@@ -94,7 +102,8 @@ class Renderer:
         n = ctypes.c_size_t()
         self._check(self._lib.frm_frame_pixels(self.ctx, int(ticket), ctypes.byref(ptr), ctypes.byref(n)))
         view = np.ctypeslib.as_array(ptr, shape=(n.value,))
-        view = view.reshape(shape or (self.height, self.width, 4))
+        shape = shape or self.__dict__.get("_ticket_shapes", {}).get(int(ticket), (self.height, self.width, 4))
+        view = view.reshape(shape)
         return view.copy() if copy else view
 
     def synchronize(self):

@@ -163,9 +163,13 @@ uint32_t frm_abi_version(void);
 int frm_device_count(int32_t* out_count);
 
 /* ---- frame size (replaces BlitGraphics::init / update_render_texture_size,
- *      graphics.rs:54-57, render_texture_config.rs:1-22). Allocates the device
- *      RGBA8 framebuffer, pitch = 4*width. The caller sets aspect_scale with
- *      frm_parameters_update_aspect(width, height) semantics (parameters.rs:18-21). */
+ *      graphics.rs:54-57, render_texture_config.rs:1-22). Sizes the device RGBA8
+ *      framebuffer(s), pitch = 4*width. The caller sets aspect_scale with
+ *      frm_parameters_update_aspect(width, height) semantics (parameters.rs:18-21).
+ *      Asynchronous: frames in flight finish at their own size and their pending
+ *      readbacks (frm_read_frame_async tickets) keep their bytes; the buffers of the new
+ *      size are allocated in stream order (no host wait), as a wgpu texture re-creation
+ *      does not stall the frames already submitted. */
 int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height);
 
 /* ---- uniform upload (replaces Graphics::update_parameters_buffer,

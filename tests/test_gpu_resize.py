@@ -29,6 +29,33 @@ def test_resize_sequence_bit_exact(frm_lib, oracle, inflight):
                 assert st["march_steps"] == int(ref["counters"][2] + ref["counters"][3])
 
 
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_resize_in_flight_loop_bit_exact(frm_lib, oracle, inflight):
+    """frm_resize does not drain: the drop-in loop (frame k rendered, its readback started, frame
+    k - inflight + 1's pixels awaited) resizes between frames while earlier frames of the old size
+    are still rendering and being read back. Every frame, before and after each size change (up
+    past the framebuffer headroom, down, the reference's +-1 factor steps), equals the oracle's."""
+    sizes = [(160, 90), (168, 94), (160, 90), (320, 180), (96, 54), (152, 86), (160, 90)]
+    frames, want = [], {}
+    for w, h in sizes:
+        p = params_for(18, 12, frm.POWER8_TIME, w, h)
+        want[(w, h)] = oracle.render(p, w, h, 256)["rgba"]
+        frames += [(w, h, p)] * 3
+    with frm.Renderer(device=0, max_steps=256, flags=frm.FRM_FLAG_PERSISTENT_KERNEL, frames_in_flight=inflight) as r:
+        held = []
+        for k, (w, h, p) in enumerate(frames):
+            if (w, h) != (r.width, r.height):
+                r.resize(w, h)
+            r.update_parameters_buffer(p)
+            r.render(stats=False)
+            held.append((k, w, h, r.read_frame_async()))
+            while len(held) > inflight - 1:
+                j, fw, fh, t = held.pop(0)
+                assert np.array_equal(r.frame_pixels(t), want[(fw, fh)]), f"frame {j} ({fw}x{fh})"
+        for j, fw, fh, t in held:
+            assert np.array_equal(r.frame_pixels(t), want[(fw, fh)]), f"frame {j} ({fw}x{fh})"
+
+
 @pytest.mark.parametrize("scene,iters", [(15, 2 ** 31 + 5), (15, 0xFFFFFFFF), (18, 5000), (0, 4100)])
 def test_num_iterations_above_old_cap(frm_lib, oracle, scene, iters):
     w, h = 32, 18
