@@ -394,9 +394,10 @@ def main():
     # 8 per launch and 2 in flight; whole 4K frame 11.20 -> 10.84 ms at 8 per launch, 1080p
     # 3.12 -> 2.80; 16 per launch: 10.42 -> 10.37 ms, 1080p 2.66 -> 2.63, 8-way share 1.416 ->
     # 1.385-1.402, profiles/round2/batch32/). Auto: the timed frames in equal launches of at
-    # most 16 (20 frames: 2 x 10). Animated workloads change the scene every frame: one frame
-    # per launch.
-    if w.moving:
+    # most 16 (20 frames: 2 x 10). Moving workloads batch too when their frames differ only in
+    # camera and the Mandelbulb's time (frm_render_bands_batch: a per-lane power), i.e. scene 18;
+    # other animated scenes change more scene constants per frame: one frame per launch.
+    if w.moving and (w.scene != 18 or w.sphere):
         batch = 1
     elif args.batch:
         batch = max(1, min(args.batch, frm.FRM_MAX_BATCH))
@@ -431,6 +432,7 @@ def main():
     main_stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(main_stream)
     kev = []  # (start, stop) HIP events around every render launch of the timed region
+    launch_params = []  # moving workloads in batches: the next launch's frames (before_frame)
     timing = {"on": False}
 
     def render_bands(buf, br, first, stride, slot, count):
@@ -439,8 +441,10 @@ def main():
         if timing["on"]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(s)
-        if batch > 1:  # one launch, `count` frames (same scene and camera here), frame b at b * tf.nbytes
-            r.render_bands_batch([params] * count, buf.data_ptr(), buf.numel(), tf.nbytes, br, first, stride,
+        if batch > 1:  # one launch, `count` frames, frame b at b * tf.nbytes
+            ps = launch_params[:count] if launch_params else [params] * count  # warmup: frame 0
+            del launch_params[:count]
+            r.render_bands_batch(ps, buf.data_ptr(), buf.numel(), tf.nbytes, br, first, stride,
                                  s.cuda_stream, counters.data_ptr())
         else:
             r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
@@ -455,12 +459,16 @@ def main():
     tf = RowTiledFrame(w.width, w.height, 0 if split == 1 else rank, split, band_rows, dev, render_bands, unshuffle,
                        inflight=inflight, streams=streams, batch=batch)
 
-    # Animated workloads (C5, HEADLINE_FLY): timed frame k renders frame k of the sequence
-    # (one frame per launch: the scene uniforms change every frame)
+    # Animated workloads (C5, HEADLINE_FLY): timed frame k renders frame k of the sequence (a
+    # launch of `batch` frames takes the next `batch` of them)
     before_frame = None
     if w.moving:
         def before_frame(k):
-            r.update_parameters_buffer(frame0 if k == 0 else next(seq))
+            p = frame0 if k == 0 else next(seq)
+            if batch > 1:
+                launch_params.append(p)
+            else:
+                r.update_parameters_buffer(p)
 
     tf.run(args.warmup)
     torch.cuda.synchronize()

@@ -852,31 +852,44 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
   if ((uint64_t)rows * ctx->width * count >= 0xFFFFFFFFull - kQueueHeadroom)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "batch of %u frames of %u x %u local pixels too large", count,
                 ctx->width, rows);
-  // frames of one launch may differ in camera only: same scene uniforms (scene, iterations,
-  // time-derived constants) and aspect
+  // frames of one launch may differ in camera, and for the Mandelbulb in time (its power,
+  // fragment.wgsl:75, is the only time-derived constant): otherwise the same scene uniforms
+  // (scene, iterations, time-derived constants) and aspect
   SceneUniforms s0;
   compute_scene_uniforms(params[0], ctx->flags, &s0);
   if (int rc = check_parameters(ctx, s0, params[0])) return rc;
+  bool anim = false;
+  float powers[FRM_MAX_BATCH];
+  powers[0] = s0.mb_power;
   for (uint32_t k = 1; k < count; ++k) {
     SceneUniforms sk;
     compute_scene_uniforms(params[k], ctx->flags, &sk);
+    powers[k] = sk.mb_power;
+    if (is_mandelbulb(s0.family) && sk.family == s0.family && sk.mb_power != s0.mb_power) {
+      anim = true;
+      sk.mb_power = s0.mb_power;
+      sk.mb_power_m1 = s0.mb_power_m1;
+    }
     if (memcmp(&s0, &sk, sizeof(s0)) != 0 || params[k].aspect_scale[0] != params[0].aspect_scale[0] ||
         params[k].aspect_scale[1] != params[0].aspect_scale[1])
       return fail(ctx, FRM_ERR_INVALID_ARGUMENT,
-                  "batch frame %u differs from frame 0 in more than the camera (scene, iterations, time, aspect)", k);
+                  "batch frame %u differs from frame 0 in more than the camera and the Mandelbulb's time "
+                  "(scene, iterations, time-derived constants, aspect)",
+                  k);
   }
   ctx->params = params[count - 1];  // the context's parameters: the batch's last frame
-  ctx->scene = s0;
+  compute_scene_uniforms(params[count - 1], ctx->flags, &ctx->scene);
   ctx->has_params = true;
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   unsigned long long* counters = dev_counters ? (unsigned long long*)dev_counters : ctx->counters;
   KernelArgs a = make_args(ctx, dev_dst, counters, band_rows, first_band, band_stride, rows);
   FrameUniforms fk;
-  if (count == 1 || kernel_for(ctx, a.npix) == kKernelSimple || ctx->reloaded) {
-    // one launch per frame (the simple kernel has no queue to share; runtime-reloaded
-    // modules carry the single-frame kernels only)
+  // one launch per frame: the simple kernel has no queue to share; runtime-reloaded modules carry
+  // the single-frame kernels only; per-frame powers need the Mandelbulb's N >= 1 kernels
+  if (count == 1 || kernel_for(ctx, a.npix) == kKernelSimple || ctx->reloaded || (anim && s0.n == 0)) {
     for (uint32_t k = 0; k < count; ++k) {
+      compute_scene_uniforms(params[k], ctx->flags, &a.s);
       compute_frame_uniforms(params[k], ctx->width, ctx->height, ctx->max_steps, &a.f);
       memcpy(a.cams[0].row, a.f.row, sizeof(a.f.row));
       a.cams[0].origin = a.f.origin;
@@ -888,6 +901,8 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
   }
   a.batch = count;
   a.out_stride = (uint32_t)(frame_stride_bytes / 4u);
+  a.anim = anim ? 1u : 0u;
+  memcpy(a.mb_powers, powers, sizeof(float) * count);
   for (uint32_t k = 0; k < count; ++k) {
     compute_frame_uniforms(params[k], ctx->width, ctx->height, ctx->max_steps, &fk);
     memcpy(a.cams[k].row, fk.row, sizeof(fk.row));

@@ -71,6 +71,11 @@ struct KernelArgs {
   uint32_t* key_hist_next;
   uint32_t* order_out;
   FrameCamera cams[kMaxBatch];
+  // Multi-frame launch of an animated Mandelbulb (frames that differ in time, hence in the power
+  // only: fragment.wgsl:75): frame k's power. Used by the ANIM instantiation of march_persistent,
+  // which carries a per-lane power; s.mb_power otherwise.
+  float mb_powers[kMaxBatch];
+  uint32_t anim;
 };
 constexpr uint32_t kRankWords = 512;  // one launch's key_hist: 256 counts + 256 cursors
 constexpr uint32_t kShadeBlockPixels = 4096;  // shade_pass / rank_pass: local pixels per 256-thread block

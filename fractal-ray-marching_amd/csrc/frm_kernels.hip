@@ -187,7 +187,15 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
     if (e != hipSuccess) return e;
     return module_launch(rk->shade[FAM], dim3(shade_blocks, args.batch), dim3(256), stream, args);
   }
-  hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+  if constexpr (is_mandelbulb(FAM) && ITERS) {
+    if (args.anim) {
+      hipLaunchKernelGGL((march_persistent<FAM, ITERS, true, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+    } else {
+      hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+    }
+  } else {
+    hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+  }
   hipLaunchKernelGGL((shade_pass<FAM>), dim3(shade_blocks, args.batch), dim3(256), 0, stream, args);
   if (args.key_hist)  // fused scheduling: the slot's next fetch order
     hipLaunchKernelGGL(rank_pass, dim3((args.npix + kShadeBlockPixels - 1u) / kShadeBlockPixels), dim3(256), 0, stream,

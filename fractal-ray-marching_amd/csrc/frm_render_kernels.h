@@ -105,7 +105,9 @@ __device__ unsigned long long g_wave_debug[16u * kWaveDebugSlots];
 // Queue chunk c (64 fetch positions) is chunk c / batch of frame c % batch: the frames'
 // pixels interleave chunk by chunk, each frame's longest first, and a chunk's frame (camera)
 // is wave-uniform.
-template <uint32_t FAM, bool ITERS, bool MULTI = false>
+// ANIM (MULTI, Mandelbulb): the frames of the launch differ in time, so in the power; each lane
+// carries its pixel's frame's power (a.mb_powers) instead of the uniform one.
+template <uint32_t FAM, bool ITERS, bool MULTI = false, bool ANIM = false>
 #ifndef FRM_MARCH_WAVES_PER_SIMD
 #define FRM_MARCH_WAVES_PER_SIMD 1
 #endif
@@ -123,6 +125,8 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   const uint32_t total = multi ? a.batch * ((a.npix + kChunk - 1u) / kChunk) * kChunk : a.npix;
   uint32_t chunk_frame = 0;  // wave-uniform: the frame of the wave's current chunk
   const uint32_t n_iter = iterations<ITERS>(su.n);
+  static_assert(!ANIM || (MULTI && is_mandelbulb(FAM)), "per-lane powers: multi-frame Mandelbulb launches");
+  float lane_power = su.mb_power;  // ANIM: the power of the lane's pixel's frame
   ShadeGeom* __restrict__ geom = a.geom;
   ShadeTail* __restrict__ tails = a.tails;
 
@@ -189,7 +193,10 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           n_dbg_total++;
           if (ballot(!mb_tame(z, mag)) != 0) n_dbg_exact++;
 #endif
-          mb_step<kHw>(su, q, mag, z, dr);
+          if constexpr (ANIM)
+            mb_step<kHw>(lane_power, lane_power - 1.0f, q, mag, z, dr);  // = the host's mb_power_m1
+          else
+            mb_step<kHw>(su, q, mag, z, dr);
           body++;
           if (body > n_iter) {
             fin = 1;  // N+1 bodies: the distance uses the last loop-top magnitude
@@ -363,6 +370,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
             pix_cost = 0;
             d = mk(r.x, r.y, r.z);
             o = multi ? a.cams[chunk_frame].origin : f.origin;
+            if constexpr (ANIM) lane_power = a.mb_powers[chunk_frame];
             t = 0.f;
             it = 0;
             phase = kPrimary;

@@ -208,9 +208,9 @@ FRM_HD float de_koch(const SceneUniforms& u, v3 p) {
 
 // One Mandelbulb loop body (fragment.wgsl:251-267) at magnitude r = length(z) <= bailout:
 // updates z and dr in place. pow(r, y) is exp2(y*log2(r)) (frm semantics), so log2(r)
-// is shared by both pows.
-FRM_HD void mb_body(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
-  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+// is shared by both pows. P = power, Pm1 = power - 1 (SceneUniforms::mb_power / mb_power_m1, or
+// one frame's of a multi-frame launch with per-frame powers).
+FRM_HD void mb_body(float P, float Pm1, v3 c, float r, v3& z, float& dr) {
   float theta = acos_(z.z / r);
   float phi = atan2_(z.y, z.x);
   float l2 = log2_(r);
@@ -262,8 +262,7 @@ __device__ __forceinline__ float hw_atan2(float y, float x) {
   r = (x < 0.0f) ? kPi - r : r;
   return copysignf(r, y);
 }
-__device__ __forceinline__ void mb_body_hw(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
-  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+__device__ __forceinline__ void mb_body_hw(float P, float Pm1, v3 c, float r, v3& z, float& dr) {
   float theta = hw_acos(hw_div(z.z, r));
   float phi = hw_atan2(z.y, z.x);
   float l2 = __builtin_amdgcn_logf(r);
@@ -328,8 +327,7 @@ __device__ __forceinline__ bool mb_tame(v3 z, float r) {
 }
 
 // mb_body (frm_scene.h) with the tame primitives: the same operations in the same order.
-__device__ __forceinline__ void mb_body_tame(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
-  const float P = u.mb_power, Pm1 = u.mb_power_m1;
+__device__ __forceinline__ void mb_body_tame(float P, float Pm1, v3 c, float r, v3& z, float& dr) {
   float theta = acos_dev(div_tame_nz(z.z, r));  // acos_dev(-0) == acos_dev(+0)
   float phi = atan2_tame(z.y, z.x);
   float l2 = log2_tame(r);
@@ -355,18 +353,22 @@ __device__ __forceinline__ bool length_small(v3 a) {
 // its active lanes have tame operands. Bit-identical to mb_body either way. HW: the hardware-
 // transcendental body (FRM_FLAG_HW_MATH; host builds have no such math and run mb_body).
 template <bool HW = false>
-FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+FRM_HD void mb_step(float P, float Pm1, v3 c, float r, v3& z, float& dr) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (HW) {
-    mb_body_hw(u, c, r, z, dr);
+    mb_body_hw(P, Pm1, c, r, z, dr);
     return;
   }
   if (ballot(!mb_tame(z, r)) == 0) {
-    mb_body_tame(u, c, r, z, dr);
+    mb_body_tame(P, Pm1, c, r, z, dr);
     return;
   }
 #endif
-  mb_body(u, c, r, z, dr);
+  mb_body(P, Pm1, c, r, z, dr);
+}
+template <bool HW = false>
+FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
+  mb_step<HW>(u.mb_power, u.mb_power_m1, c, r, z, dr);
 }
 // length(z) for the Mandelbulb magnitude; fast sqrt unless a lane has 0 < |z|^2 < 2^-96.
 template <bool HW = false>

@@ -131,6 +131,12 @@ class RowTiledFrame:
                 for j in range(count):
                     before_frame(done + j)
             done += count
+            if pending is not None and pending[0] % self.nbuf == k % self.nbuf:
+                # one buffer set (nbuf 1): the previous launch is reassembled and captured in
+                # stream order before this launch overwrites its buffer
+                self._finish(*pending)
+                self._capture(pending[0], capture)
+                pending = None
             work = self._issue(k, count)
             if pending is not None:
                 self._finish(*pending)

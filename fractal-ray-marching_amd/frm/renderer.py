@@ -139,7 +139,8 @@ class Renderer:
 
     def render_bands_batch(self, params_list, dev_ptr, dst_bytes, frame_stride, band_rows, first_band, band_stride,
                            stream=0, dev_counters=0):
-        """frm_render_bands_batch: len(params_list) frames (same scene, camera may differ) in
+        """frm_render_bands_batch: len(params_list) frames (same scene; the camera, and for the
+        Mandelbulb the time, may differ) in
         one launch, frame k at dev_ptr + k * frame_stride; dst_bytes = the size of the buffer at
         dev_ptr (the library checks every frame against it: pass the real allocation, e.g.
         tensor.numel(), never a size derived from the stride)."""

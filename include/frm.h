@@ -262,9 +262,11 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
  * (each frame's pixels longest first, the frames interleaved), so one frame's longest pixels
  * run beside the other frames' work instead of ending a launch with idle lanes: for short
  * launches (a rank's share of a row-split frame) the persistent kernel's tail is paid once
- * per batch. The frames may differ in camera only: params[k] must give the same scene,
- * num_iterations, time-derived scene constants and aspect as params[0]
- * (FRM_ERR_INVALID_ARGUMENT otherwise). The context's parameters become params[count-1].
+ * per batch. The frames may differ in camera, and the Mandelbulb's (scene 18) in time too (its
+ * power is its one time-derived constant, fragment.wgsl:75; each lane then carries its frame's
+ * power): otherwise params[k] must give the same scene, num_iterations, time-derived scene
+ * constants and aspect as params[0] (FRM_ERR_INVALID_ARGUMENT otherwise). A scripted
+ * fly-through (the CLI's, bench.py's HEADLINE_FLY) so renders several of its frames per launch. The context's parameters become params[count-1].
  * Counters are added over all frames. Bytes per frame are those of frm_render_bands; dev_dst
  * holds dst_bytes bytes, at least (count - 1) * frame_stride_bytes + one frame's bands
  * (FRM_ERR_BUFFER_TOO_SMALL otherwise); frame_stride_bytes is a multiple of 4 below 16 GiB. */

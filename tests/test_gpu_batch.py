@@ -73,18 +73,23 @@ def test_batch_band_split_bit_exact(frm_lib, oracle):
 
 
 def test_batch_rejects_frames_that_differ_beyond_the_camera(frm_lib):
+    """A batch's frames share the scene uniforms, except the Mandelbulb's power (its only
+    time-derived constant): another iteration count, another scene, or another time of an
+    animated Menger scene is refused."""
     import torch
 
     w, h = 32, 18
     a = params_for(18, 12, frm.POWER8_TIME, w, h)
-    b = params_for(18, 12, frm.POWER8_TIME + 1.0, w, h)  # another time: another power
-    c = params_for(18, 11, frm.POWER8_TIME, w, h)        # other iteration count
+    c = params_for(18, 11, frm.POWER8_TIME, w, h)  # other iteration count
+    m0 = params_for(4, 3, 0.5, w, h)               # animated Menger: the time moves its cross size
+    m1 = params_for(4, 3, 1.5, w, h)
+    d = params_for(0, 12, frm.POWER8_TIME, w, h)   # another scene
     buf = torch.zeros(2 * w * h * 4, dtype=torch.uint8, device="cuda")
     with frm.Renderer(device=0, max_steps=64) as r:
         r.resize(w, h)
-        for other in (b, c):
+        for first, other in ((a, c), (m0, m1), (a, d)):
             with pytest.raises(frm.FrmError) as e:
-                r.render_bands_batch([a, other], buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
+                r.render_bands_batch([first, other], buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
             assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
         with pytest.raises(frm.FrmError):
             r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
@@ -141,3 +146,40 @@ def test_batch_rank_without_bands(frm_lib):
             r.render_bands_batch([a] * 3, buf.data_ptr(), nbytes, stride, br, 1, ranks, 0, counters.data_ptr())
         torch.cuda.synchronize()
         assert int(counters.sum()) == 0 and int(buf.sum()) == 0
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "simple"])
+def test_batch_animated_mandelbulb_bit_exact(frm_lib, oracle, kernel):
+    """Frames of a fly-through whose time advances (frm.frame_sequence sped up 20x: the Mandelbulb's
+    power moves every frame) in multi-frame launches of 3, two launches in flight: each lane
+    carries its frame's power (the ANIM instantiation; the simple kernel renders frame by frame).
+    Every frame equals the oracle's render of its own Parameters; a launch's counters are the sum
+    of its frames'."""
+    import torch
+
+    w = frm.WORKLOADS["HEADLINE_FLY"]
+    width, height, B = 160, 90, 3
+    seq = frm.frame_sequence(w, pose="P1", dt=20 * frm.FRAME_SECONDS)
+    frames = [next(seq) for _ in range(3 * B)]
+    assert len({p.time for p in frames}) == len(frames)
+    for p in frames:
+        p.update_aspect(width, height)
+    refs = [oracle.render(p, width, height, 256) for p in frames]
+    nb = width * height * 4
+    flags = frm.FRM_FLAG_PERSISTENT_KERNEL if kernel == "persistent" else frm.FRM_FLAG_SIMPLE_KERNEL
+    bufs = [torch.zeros(B * nb, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with frm.Renderer(device=0, max_steps=256, flags=flags, frames_in_flight=2) as r:
+        r.resize(width, height)
+        for launch in range(3):
+            ps = frames[launch * B:(launch + 1) * B]
+            buf = bufs[launch % 2]
+            counters.zero_()
+            r.render_bands_batch(ps, buf.data_ptr(), buf.numel(), nb, height, 0, 1, 0, counters.data_ptr())
+            r.synchronize()
+            got = buf.cpu().numpy()
+            for b in range(B):
+                k = launch * B + b
+                assert np.array_equal(got[b * nb:(b + 1) * nb].reshape(height, width, 4), refs[k]["rgba"]), f"frame {k}"
+            want = sum(np.asarray(refs[launch * B + b]["counters"], dtype=np.int64) for b in range(B))
+            assert np.array_equal(counters.cpu().numpy()[:7], want[:7]), f"launch {launch}"

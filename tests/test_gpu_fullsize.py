@@ -150,6 +150,36 @@ def test_fly_through_sequence_matches_golden(frm_lib):
             assert hashlib.sha256(r.read_frame().tobytes()).hexdigest() == g[key]["sha256"], key
 
 
+def test_fly_through_batched_matches_golden(frm_lib):
+    """The same frames 0, 1, 2 of HEADLINE_FLY in ONE multi-frame launch (the time, hence the
+    Mandelbulb's power, and the camera differ per frame; bench.py renders the fly-through so), on a
+    context whose previous launch was the same batch (scheduled order): every frame matches its
+    golden hash and the launch's counters are the three frames' sums."""
+    import hashlib
+
+    import torch
+
+    g = _golden()
+    w = frm.WORKLOADS["HEADLINE_FLY"]
+    seq = frm.frame_sequence(w, pose="P1")
+    keys = ("HEADLINE_P1", "HEADLINE_FLY_P1_f1", "HEADLINE_FLY_P1_f2")
+    ps = [next(seq) for _ in keys]
+    nb = w.width * w.height * 4
+    buf = torch.zeros(len(keys) * nb, dtype=torch.uint8, device="cuda")
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with frm.Renderer(device=0, max_steps=w.max_steps, frames_in_flight=1) as r:
+        r.resize(w.width, w.height)
+        for rep in range(2):
+            counters.zero_()
+            r.render_bands_batch(ps, buf.data_ptr(), buf.numel(), nb, w.height, 0, 1, 0, counters.data_ptr())
+            r.synchronize()
+            host = buf.cpu().numpy()
+            for b, key in enumerate(keys):
+                assert hashlib.sha256(host[b * nb:(b + 1) * nb].tobytes()).hexdigest() == g[key]["sha256"], (rep, key)
+            want = [sum(g[k]["counters"][i] for k in keys) for i in range(7)]
+            assert counters.cpu().tolist()[:7] == want, rep
+
+
 def _split_frames(name, ranks, params_list, batch, inflight):
     """bench.py's --split rows data path for `ranks` ranks, simulated on one device: one context
     per rank (frames_in_flight = inflight); the frames of params_list in launches of `batch`
