@@ -28,11 +28,12 @@ def read_ppm(path):
     return np.frombuffer(pix, np.uint8).reshape(h, w, 3)
 
 
-@pytest.mark.parametrize("gpus", [0, 1], ids=["one-context", "rccl-row-tiled"])
-def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib, gpus):
+@pytest.mark.parametrize("gpus,batch", [(0, 1), (1, 1), (0, 2)], ids=["one-context", "rccl-row-tiled", "batched"])
+def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib, gpus, batch):
     """gpus=1: the CLI's C host multi-GPU path (ncclCommInitAll, interleaved bands per device
     via frm_render_bands, RCCL send/recv gather on device 0, frm_unshuffle_bands) with the
-    one device this box has; N > 1 runs the same code with more ranks."""
+    one device this box has; N > 1 runs the same code with more ranks. batch=2: frames 0-1 in
+    one frm_render_bands_batch launch (time and camera differ), frame 2 in another."""
     W, H, frames, dt, keys, orbit = 96, 54, 3, 0.05, frm.HeldKeys.MOVE_FORWARD | frm.HeldKeys.YAW_LEFT, 2.0
     pos, iters, time, steps = (1.5, 0.9, -1.5), 6, frm.POWER8_TIME, 256
     out = str(tmp_path / "f_%02d.ppm")
@@ -41,6 +42,8 @@ def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib, gpus):
            "--iters", str(iters), "--time", str(time), "--max-steps", str(steps), "--scene", "18", "--out", out]
     if gpus:
         cmd += ["--gpus", str(gpus)]
+    if batch > 1:
+        cmd += ["--batch", str(batch)]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert res.returncode == 0, res.stderr
     lines = [json.loads(l) for l in res.stdout.splitlines() if l.startswith("{")]
@@ -55,6 +58,7 @@ def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib, gpus):
     cam.raw.lock_pitch = 1
     timing = frm.Timing()
     p.update_camera(cam)
+    launch = {}
     for fr in range(frames):
         if fr > 0:
             delta = timing.update(p, dt)
@@ -64,5 +68,12 @@ def test_cli_flythrough_matches_oracle(tmp_path, oracle, frm_lib, gpus):
         ref = oracle.render(p, W, H, steps)
         got = read_ppm(out % fr)
         assert np.array_equal(got, ref["rgba"][..., :3]), f"frame {fr}"
-        assert lines[fr]["march_steps"] == int(ref["counters"][2]) + int(ref["counters"][3])
-        assert lines[fr]["hit_pixels"] == int(ref["counters"][1])
+        if batch == 1:
+            assert lines[fr]["march_steps"] == int(ref["counters"][2]) + int(ref["counters"][3])
+            assert lines[fr]["hit_pixels"] == int(ref["counters"][1])
+        else:  # the launch's counters: the sum over its frames
+            g = launch.setdefault(fr // batch, [0, 0, lines[fr]])
+            g[0] += int(ref["counters"][2]) + int(ref["counters"][3])
+            g[1] += int(ref["counters"][1])
+    for steps_sum, hits_sum, line in launch.values():
+        assert line["launch_march_steps"] == steps_sum and line["launch_hit_pixels"] == hits_sum
