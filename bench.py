@@ -176,10 +176,19 @@ def pmc_summary(workload, world):
             if sh.get("source_sha256") == cur:
                 shade = (sh["hbm_read_bytes"] + sh["hbm_write_bytes"]) / sh.get("frames_per_dispatch", 1)
                 shade_src = os.path.relpath(spath, ROOT)
+        # rank_pass (fused scheduling): once per launch, i.e. per B frames of the march's dispatch
+        rank = None
+        rpath = path.replace("_march.json", "_rank.json")
+        if os.path.exists(rpath):
+            with open(rpath) as fh:
+                rk = json.load(fh)
+            if rk.get("source_sha256") == cur and "hbm_read_bytes" in rk:
+                rank = (rk["hbm_read_bytes"] + rk["hbm_write_bytes"]) / B
+                shade_src = (shade_src + " + " if shade_src else "") + os.path.relpath(rpath, ROOT)
         return {
-            # HBM bytes per frame (a dispatch renders B frames): march + shade, and the split
-            "traffic": march + (shade or 0.0),
-            "traffic_split": {"march_persistent": march, "shade_pass": shade},
+            # HBM bytes per frame (a dispatch renders B frames): march + shade + rank, and the split
+            "traffic": march + (shade or 0.0) + (rank or 0.0),
+            "traffic_split": {"march_persistent": march, "shade_pass": shade, "rank_pass": rank},
             "valu_busy": s["valu_busy"],
             "valu_lane_utilization": s["valu_lane_utilization"],
             "hbm_write_gbps": s["hbm_write_gbps"],
@@ -402,8 +411,13 @@ def main():
     elif args.batch:
         batch = max(1, min(args.batch, frm.FRM_MAX_BATCH))
     else:
+        # one GPU: up to FRM_MAX_BATCH per launch (30 frames in one launch against 2 x 15 after
+        # fused scheduling: headline 10.11-10.18 -> 10.10-10.12 ms, C3 1.01-1.04 -> 0.99-1.00, C2
+        # equal, fly-through 10.66-10.77 -> 10.57-10.58; profiles/round4/batch_sweep); a row split
+        # keeps launches of at most 16 so one launch's gather overlaps the next launch's render
+        cap = frm.FRM_MAX_BATCH if split == 1 else 16
         k = max(1, args.steps)
-        batch = -(-k // -(-k // 16))
+        batch = -(-k // -(-k // cap))
     if args.inflight:
         inflight = args.inflight
     elif batch > 1:

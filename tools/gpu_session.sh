@@ -17,9 +17,11 @@ tests)
   tail -1 "$OUT/pytest_gpu.log"
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail "$OUT/smoke.log"; exit 1; }
   tail -1 "$OUT/smoke.log"
-  timeout -k 10 400 python bench.py --steps 20 --warmup 5 > "$OUT/bench_HEADLINE.json" 2> "$OUT/bench.err" || { tail "$OUT/bench.err"; exit 1; }
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-dropin > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { tail "$OUT/prof.err"; exit 1; }
-  python tools/rocprof_timed.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" 2 10 > "$OUT/rocprof_timed_HEADLINE.txt"
+  # the driver's command (defaults: 30 timed frames, one launch of 30 on one GPU)
+  timeout -k 10 400 python bench.py > "$OUT/bench_HEADLINE.json" 2> "$OUT/bench.err" || { tail "$OUT/bench.err"; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-dropin > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { tail "$OUT/prof.err"; exit 1; }
+  B=$(python3 -c "import json;print(json.load(open('$OUT/prof_bench.json'))['config']['frames_per_launch'])")
+  python tools/rocprof_timed.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" 1 "$B" > "$OUT/rocprof_timed_HEADLINE.txt"
   cp "$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1)" "$OUT/rocprof_kernel_stats_HEADLINE.csv"
   echo TESTS_OK ;;
 configs)
@@ -30,21 +32,21 @@ configs)
   done
   echo CONFIGS_OK ;;
 pmc)
-  # PMC_SPECS: "WORKLOAD:bench args" entries separated by '|' (default: every config); SHARE8=1 adds
-  # one rank's share of the 8-way split. tools/pmc_summary.py averages the dispatches after the first
-  # two: the defaults give every averaged dispatch the same frames per launch (fixed workloads: 16 or 4
-  # per launch, 2 averaged; C5, animated: 1 per launch, 4 averaged)
-  IFS='|' read -r -a specs <<< "${PMC_SPECS:-HEADLINE:--steps 48 --warmup 16 --batch 16|C2:--steps 48 --warmup 16 --batch 16|C3:--steps 48 --warmup 16 --batch 16|C4:--steps 12 --warmup 4 --batch 4|C5:--steps 4 --warmup 2}"
+  # PMC_SPECS: "WORKLOAD:bench args" entries separated by '|' (default: every config and the batched
+  # fly-through); SHARE8=1 adds one rank's share of the 8-way split. tools/pmc_summary.py averages the
+  # dispatches after the first two: the defaults give every averaged dispatch the same frames per
+  # launch (16 or 4 per launch, 2 averaged; C5, animated and batched: 3 per launch, 2 averaged)
+  IFS='|' read -r -a specs <<< "${PMC_SPECS:-HEADLINE:--steps 48 --warmup 16 --batch 16|HEADLINE_FLY:--steps 48 --warmup 16 --batch 16|C2:--steps 48 --warmup 16 --batch 16|C3:--steps 48 --warmup 16 --batch 16|C4:--steps 12 --warmup 4 --batch 4|C5:--steps 9 --warmup 3 --batch 3}"
   for spec in "${specs[@]}"; do
     wl=${spec%%:*}; a=${spec#*:}
     OUT="$OUT/pmc_raw/$wl" ARGS="--workload $wl $a --no-cpu-baseline --no-dropin" bash tools/pmc.sh > /dev/null || { echo "pmc $wl failed"; exit 1; }
-    python tools/pmc_summary.py "$OUT/pmc_raw/$wl" > "$OUT/pmc_${wl}_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/$wl" shade_pass > "$OUT/pmc_${wl}_shade.json" || exit 1
+    python tools/pmc_summary.py "$OUT/pmc_raw/$wl" > "$OUT/pmc_${wl}_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/$wl" shade_pass > "$OUT/pmc_${wl}_shade.json" && python tools/pmc_summary.py "$OUT/pmc_raw/$wl" rank_pass > "$OUT/pmc_${wl}_rank.json" || exit 1
     python -c "import json;s=json.load(open('$OUT/pmc_${wl}_march.json'));print('$wl', 'valu_busy', round(s['valu_busy'],3), 'lane_util', round(s['valu_lane_utilization'],3), 'valu_insts/frame %.3g' % (s['valu_wave_insts']/s['frames_per_dispatch']), 'sq3', s.get('sq3'))"
   done
   if [ -n "$SHARE8" ]; then
     # one rank's share of bench.py's 8-way row split (rank 0, 2 launches in flight, 10 frames per launch)
     OUT="$OUT/pmc_raw/HEADLINE_share8" PROG=tools/pipeline_probe.py ARGS="--workloads HEADLINE --ranks 8 --inflight 2 --batch 10 --frames 40" bash tools/pmc.sh > /dev/null || { echo "pmc share8 failed"; exit 1; }
-    python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" > "$OUT/pmc_HEADLINE_share8_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" shade_pass > "$OUT/pmc_HEADLINE_share8_shade.json" || exit 1
+    python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" > "$OUT/pmc_HEADLINE_share8_march.json" && python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" shade_pass > "$OUT/pmc_HEADLINE_share8_shade.json" && python tools/pmc_summary.py "$OUT/pmc_raw/HEADLINE_share8" rank_pass > "$OUT/pmc_HEADLINE_share8_rank.json" || exit 1
   fi
   echo PMC_OK ;;
 *) echo "PART=tests|configs|pmc"; exit 2 ;;

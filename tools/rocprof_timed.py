@@ -15,7 +15,7 @@ import sys
 
 def kind(n):
     return ("march_persistent" if "march_persistent" in n else "shade_pass" if "shade_pass" in n
-            else "radix_sort" if "radix_sort" in n else None)
+            else "rank_pass" if "rank_pass" in n else "radix_sort" if "radix_sort" in n else None)
 
 
 def main(trace, k, batch=1):
@@ -30,7 +30,7 @@ def main(trace, k, batch=1):
         per[name].append((e - s) / 1e6)
     calls = len(per["march_persistent"])
     total = 0.0
-    for name in ("march_persistent", "radix_sort", "shade_pass"):
+    for name in ("march_persistent", "radix_sort", "shade_pass", "rank_pass"):
         d = per.get(name, [])
         per_frame = len(d) // max(calls, 1) if calls else 1  # radix sort: several dispatches per frame
         last = d[-k * max(per_frame, 1):]
