@@ -406,7 +406,9 @@ def main():
     # most 16 (20 frames: 2 x 10). Moving workloads batch too when their frames differ only in
     # camera and the Mandelbulb's time (frm_render_bands_batch: a per-lane power), i.e. scene 18;
     # other animated scenes change more scene constants per frame: one frame per launch.
-    if w.moving and (w.scene != 18 or w.sphere):
+    # (C5's 16384^2 frames: a launch's tail is ~1 % of a frame; 3 per launch measured 682 ms/frame
+    # against 634 at one per launch, profiles/round4/final/configs)
+    if w.moving and (w.scene != 18 or w.sphere or local_pixels > 64_000_000):
         batch = 1
     elif args.batch:
         batch = max(1, min(args.batch, frm.FRM_MAX_BATCH))

@@ -35,8 +35,8 @@ pmc)
   # PMC_SPECS: "WORKLOAD:bench args" entries separated by '|' (default: every config and the batched
   # fly-through); SHARE8=1 adds one rank's share of the 8-way split. tools/pmc_summary.py averages the
   # dispatches after the first two: the defaults give every averaged dispatch the same frames per
-  # launch (16 or 4 per launch, 2 averaged; C5, animated and batched: 3 per launch, 2 averaged)
-  IFS='|' read -r -a specs <<< "${PMC_SPECS:-HEADLINE:--steps 48 --warmup 16 --batch 16|HEADLINE_FLY:--steps 48 --warmup 16 --batch 16|C2:--steps 48 --warmup 16 --batch 16|C3:--steps 48 --warmup 16 --batch 16|C4:--steps 12 --warmup 4 --batch 4|C5:--steps 9 --warmup 3 --batch 3}"
+  # launch (16 or 4 per launch, 2 averaged; C5, animated: 1 per launch, 4 averaged)
+  IFS='|' read -r -a specs <<< "${PMC_SPECS:-HEADLINE:--steps 48 --warmup 16 --batch 16|HEADLINE_FLY:--steps 48 --warmup 16 --batch 16|C2:--steps 48 --warmup 16 --batch 16|C3:--steps 48 --warmup 16 --batch 16|C4:--steps 12 --warmup 4 --batch 4|C5:--steps 4 --warmup 2}"
   for spec in "${specs[@]}"; do
     wl=${spec%%:*}; a=${spec#*:}
     OUT="$OUT/pmc_raw/$wl" ARGS="--workload $wl $a --no-cpu-baseline --no-dropin" bash tools/pmc.sh > /dev/null || { echo "pmc $wl failed"; exit 1; }
