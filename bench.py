@@ -4,8 +4,10 @@
 Workload (BASELINE.json metric): 3840x2160 Mandelbulb (scene 18 at power 8), 12 DE
 iterations, 256 march steps, fixed camera pose P1; one "step" = one whole frame of the
 hot path (fragment_main for every pixel) with inputs resident on the GPU. Frames are
-rendered several per launch (--batch; frm_render_bands_batch): every frame is computed in
-full, the frames' pixels share one work queue so a launch's tail is paid once per batch.
+rendered several per launch (--batch; frm_render_bands_batch; by default on one GPU all timed
+frames, up to 32, in one launch): every frame is computed in full, the frames' pixels share one
+work queue so a launch's tail is paid once per batch. The moving HEADLINE_FLY batches too (its
+frames differ in camera and in the Mandelbulb's time: each lane carries its frame's power).
 
 N GPUs (one process each): launched by torch.distributed.run (the driver's multi-GPU runs),
 or, when no launcher set WORLD_SIZE, bench.py starts `torch.distributed.run` itself as a child
