@@ -211,10 +211,12 @@ def dropin_loop(frm, torch, w, args, flags, local, camera):
       persistent_graphics.rs:158-162): render frame k, start its readback
       (frm_read_frame_async), then wait for frame k-1's pixels (frm_frame_pixels);
     * dropin_sync: frames_in_flight = 1 and a wait for every frame before the next.
-    Untimed: 2 frames of frame 0. Timed: min(--steps, 20) frames. The march steps come from a
-    second, untimed pass over the same frames with stats."""
+    Untimed: 2 frames of frame 0. Timed: min(--steps, 30) frames, the bench's own frame count by
+    default (the loop's fill and drain weigh 1/n: HEADLINE_FLY 12.2 ms/frame over 20 frames,
+    12.04-12.05 over 30, profiles/round4/dropin_sm). The march steps come from a second, untimed
+    pass over the same frames with stats."""
     seq = frm.frame_sequence(w, pose=args.pose, camera=camera)
-    n = max(1, min(args.steps, 20))
+    n = max(1, min(args.steps, 30))
     frames = [next(seq) for _ in range(n)] if w.moving else [next(seq)] * n
     out = {}
     for name, fif, lag in (("dropin", 2, 1), ("dropin_sync", 1, 0)):
