@@ -464,8 +464,8 @@ def main():
         if batch > 1:  # one launch, `count` frames, frame b at b * tf.nbytes
             ps = launch_params[:count] if launch_params else [params] * count  # warmup: frame 0
             del launch_params[:count]
-            r.render_bands_batch(ps, buf.data_ptr(), buf.numel(), tf.nbytes, br, first, stride,
-                                 s.cuda_stream, counters.data_ptr())
+            r.render_bands_batch(ps, buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=tf.nbytes, band_rows=br, first_band=first, band_stride=stride,
+                                 stream=s.cuda_stream, dev_counters=counters.data_ptr())
         else:
             r.render_bands(buf.data_ptr(), buf.numel(), br, first, stride, s.cuda_stream, counters.data_ptr())
         if ev is not None:

@@ -4,6 +4,7 @@
 // Errors never cross the ABI as exceptions/aborts: every HIP failure becomes a status
 // code plus a message retrievable with frm_last_error().
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <stdarg.h>
 #include <stdio.h>
@@ -87,8 +88,37 @@ struct Slot {
   size_t copy_bytes = 0;
 };
 
+// A group context (frm_config.device_count): the context itself renders rank 0's bands on
+// devices[0] and holds the frames; sub[r] (r >= 1) renders rank r's bands on devices[r]. Per frame
+// slot: rank r's band buffer on its device, and on device 0 the rank-major gather buffer (rank 0's
+// bands are rendered straight into its first part) that frm_unshuffle_bands' kernel reassembles
+// into the slot's framebuffer.
+struct GroupSlot {
+  uint8_t* bands[FRM_MAX_DEVICES] = {};  // r >= 1 (device r's pool)
+  size_t bands_cap[FRM_MAX_DEVICES] = {};
+  hipEvent_t sent[FRM_MAX_DEVICES] = {};  // r >= 1, device r: after the slot's last gather read bands[r]
+  hipEvent_t rendered[FRM_MAX_DEVICES] = {};  // r >= 1, device r: the bands are written (copy transport)
+  hipEvent_t copied = nullptr;            // device 0: after the copy transport's gather
+  bool gather_pending = false;
+  uint8_t* gathered = nullptr;  // device 0 (context pool): ranks x stride bytes
+  size_t gathered_cap = 0;
+};
+struct Group {
+  uint32_t n = 0;
+  frm_ctx* sub[FRM_MAX_DEVICES] = {};  // sub[0] unused: rank 0 is the group context itself
+  ncclComm_t comm[FRM_MAX_DEVICES] = {};
+  bool rccl = false;  // RCCL point-to-point gather (distinct devices); else device-to-device copies
+  hipEvent_t comm_done[FRM_MAX_DEVICES] = {};  // device r: after the last gather's RCCL operations
+  bool comm_pending = false;
+  uint32_t band_rows = 0;
+  size_t stride = 0;  // bytes of rank 0's bands (the largest share): the gather buffer's rank stride
+  GroupSlot slots[FRM_MAX_FRAMES_IN_FLIGHT];
+};
+
 struct frm_ctx {
   int device = 0;
+  Group* group = nullptr;   // a group context (frm_config.device_count >= 1)
+  bool bands_only = false;  // a group's rank r >= 1: renders bands, holds no frame
   uint32_t max_steps = FRM_DEFAULT_MAX_STEPS;
   uint32_t flags = 0;
   int cu_count = 0;
@@ -146,6 +176,21 @@ int hip_fail(frm_ctx* ctx, hipError_t e, const char* what) {
     hipError_t e_ = (call);                             \
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
   } while (0)
+
+#define FRM_NCCL(ctx, call)                                                                         \
+  do {                                                                                              \
+    ncclResult_t r_ = (call);                                                                       \
+    if (r_ != ncclSuccess) return fail(ctx, FRM_ERR_HIP, "%s failed: %s", #call, ncclGetErrorString(r_)); \
+  } while (0)
+
+// A failure of a group's member context, reported on the group context.
+int relay(frm_ctx* ctx, const frm_ctx* member, int rc) {
+  return member == ctx ? rc : fail(ctx, rc, "device %d: %s", member->device, member->error.c_str());
+}
+
+int not_on_group(frm_ctx* ctx, const char* what) {
+  return fail(ctx, FRM_ERR_UNSUPPORTED, "%s: not available on a group context (frm_config.device_count)", what);
+}
 
 // Device memory of the context pool, allocated / released in the order of stream s: a block
 // released on s is reused only by work ordered after everything enqueued on s before the release.
@@ -278,16 +323,20 @@ int synchronize_all(frm_ctx* ctx) {
 
 // The stream frm_render uses for slot i (created on first use: a context with one frame in
 // flight never creates more than the context stream).
-// Slots > 0 get a stream on a hardware queue of its own: HIP maps streams onto at most
+// Slots > 0 need a hardware queue of their own to overlap: HIP maps streams onto at most
 // GPU_MAX_HW_QUEUES queues per process (4 by default) and hands the least-used one out again,
-// and two frames whose streams share a queue never overlap. The runtime
-// never pools CU-masked queues, so a stream created with a mask of every CU (no restriction) has
-// its own queue whatever the host's queue limit and other streams; plain stream as a fallback.
+// and two frames whose streams share a queue never overlap. Plain
+// non-blocking streams get distinct queues while the pool has room (bench.py raises the limit to
+// 16); FRM_SLOT_STREAMS=cumask asks for CU-masked streams, which the runtime never pools.
 hipStream_t own_queue_stream(int device) {
   hipDeviceProp_t prop;
-  const char* kind = getenv("FRM_SLOT_STREAMS");  // experiments: "plain" = pooled non-blocking stream
-  const bool plain = kind && strcmp(kind, "plain") == 0;
-  if (!plain && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
+  // default: a pooled non-blocking stream. "cumask": a CU-masked stream, which gets a hardware queue
+  // of its own but is a BLOCKING stream (hipExtStreamCreateWithCUMask takes no flags): it
+  // synchronises with the legacy null stream (torch's default stream, synchronous hipMemcpy), so
+  // it is opt-in for hosts that never use that stream
+  const char* kind = getenv("FRM_SLOT_STREAMS");
+  const bool cumask = kind && strcmp(kind, "cumask") == 0;
+  if (cumask && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
     const uint32_t words = (uint32_t)(prop.multiProcessorCount + 31) / 32u;
     uint32_t mask[64];
     if (words <= 64u) {
@@ -440,6 +489,160 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   return FRM_OK;
 }
 
+// Band height of a group's row split: the smallest height >= 16 that splits the frame into a
+// multiple of n bands (else 16), so interleaved bands balance the devices (frm/tiling.py).
+uint32_t group_band_rows(uint32_t height, uint32_t n) {
+  for (uint32_t br = 16; br <= height; ++br)
+    if (height % br == 0 && (height / br) % n == 0) return br;
+  return 16;
+}
+
+frm_ctx* member(frm_ctx* ctx, uint32_t r) { return r == 0 ? ctx : ctx->group->sub[r]; }
+
+// One frame of a group context: every device renders its interleaved bands on the stream of its
+// next frame slot (frames in flight overlap as on one device), the bands meet on device 0 (RCCL
+// grouped send/receive over xGMI, or device-to-device copies for a repeated device), and device 0
+// reassembles the frame into the slot's framebuffer on the same stream; the slot's `done` event
+// then covers the whole frame for frm_read_frame / frm_present and their async forms.
+int group_render(frm_ctx* ctx, frm_stats* stats) {
+  Group& G = *ctx->group;
+  const uint32_t n = G.n;
+  int rc = FRM_OK;
+  if (stats)  // the counters must hold this frame alone
+    for (uint32_t r = 0; r < n; ++r) {
+      frm_ctx* c = member(ctx, r);
+      FRM_HIP(ctx, hipSetDevice(c->device));
+      if ((rc = synchronize_all(c))) return relay(ctx, c, rc);
+    }
+  const uint32_t si = ctx->next_slot;
+  Slot& sl = ctx->slots[si];
+  GroupSlot& gs = G.slots[si];
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st[FRM_MAX_DEVICES];
+  if ((rc = slot_stream(ctx, si, &st[0]))) return rc;
+  const hipStream_t s0 = st[0];
+  if ((rc = select_fb(ctx, sl, sl.fb_idx ^ 1u))) return rc;
+  const size_t fb_bytes = (size_t)ctx->width * ctx->height * 4u;
+  if ((rc = ensure_fb(ctx, sl, fb_bytes + fb_bytes / 4u))) return rc;
+  const size_t gather_bytes = (size_t)n * G.stride;
+  if (gather_bytes > gs.gathered_cap) {  // its last use (this slot's last frame) is ordered before, on s0
+    if ((rc = dev_release(ctx, gs.gathered, s0))) return rc;
+    gs.gathered = nullptr;
+    gs.gathered_cap = 0;
+    if ((rc = dev_alloc(ctx, (void**)&gs.gathered, gather_bytes, s0))) return rc;
+    gs.gathered_cap = gather_bytes;
+  }
+  if (stats) {
+    FRM_HIP(ctx, hipMemsetAsync(ctx->counters, 0, FRM_NUM_COUNTERS * sizeof(unsigned long long), s0));
+    FRM_HIP(ctx, hipEventRecord(ctx->ev_start, s0));
+  }
+  uint32_t rows[FRM_MAX_DEVICES];
+  for (uint32_t r = 0; r < n; ++r) rows[r] = band_local_rows(ctx->height, G.band_rows, r, n);
+  // ranks 1..n-1 on their devices
+  for (uint32_t r = 1; r < n; ++r) {
+    frm_ctx* c = G.sub[r];
+    if (rows[r] == 0) continue;  // a frame of fewer bands than devices
+    FRM_HIP(ctx, hipSetDevice(c->device));
+    if ((rc = slot_stream(c, c->next_slot, &st[r]))) return relay(ctx, c, rc);
+    // the band buffer's last gather (this slot's last frame) has read it
+    if (gs.gather_pending)
+      FRM_HIP(ctx, hipStreamWaitEvent(st[r], G.rccl ? gs.sent[r] : gs.copied, 0));
+    if (gs.bands_cap[r] < G.stride) {
+      if ((rc = dev_release(c, gs.bands[r], st[r]))) return relay(ctx, c, rc);
+      gs.bands[r] = nullptr;
+      gs.bands_cap[r] = 0;
+      if ((rc = dev_alloc(c, (void**)&gs.bands[r], G.stride, st[r]))) return relay(ctx, c, rc);
+      gs.bands_cap[r] = G.stride;
+    }
+    if (stats) FRM_HIP(ctx, hipMemsetAsync(c->counters, 0, FRM_NUM_COUNTERS * sizeof(unsigned long long), st[r]));
+    KernelArgs a = make_args(c, gs.bands[r], c->counters, G.band_rows, r, n, rows[r]);
+    if ((rc = launch(c, a, st[r]))) return relay(ctx, c, rc);
+  }
+  // rank 0, into the first part of the gather buffer
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  KernelArgs a0 = make_args(ctx, gs.gathered, ctx->counters, G.band_rows, 0, n, rows[0]);
+  if ((rc = launch(ctx, a0, s0))) return rc;
+  // gather on device 0, rank-major
+  if (G.rccl) {
+    // one communicator, so its operations run in issue order on every device: each frame's
+    // transfers wait for the previous frame's (frames in flight use other streams)
+    if (G.comm_pending)
+      for (uint32_t r = 0; r < n; ++r) {
+        if (r > 0 && rows[r] == 0) continue;
+        FRM_HIP(ctx, hipSetDevice(member(ctx, r)->device));
+        FRM_HIP(ctx, hipStreamWaitEvent(st[r], G.comm_done[r], 0));
+      }
+    FRM_NCCL(ctx, ncclGroupStart());
+    for (uint32_t r = 1; r < n; ++r) {
+      const size_t bytes = (size_t)rows[r] * ctx->width * 4u;
+      if (!bytes) continue;
+      FRM_HIP(ctx, hipSetDevice(G.sub[r]->device));
+      FRM_NCCL(ctx, ncclSend(gs.bands[r], bytes, ncclUint8, 0, G.comm[r], st[r]));
+      FRM_HIP(ctx, hipSetDevice(ctx->device));
+      FRM_NCCL(ctx, ncclRecv(gs.gathered + (size_t)r * G.stride, bytes, ncclUint8, (int)r, G.comm[0], s0));
+    }
+    FRM_NCCL(ctx, ncclGroupEnd());
+    for (uint32_t r = 0; r < n; ++r) {
+      if (r > 0 && rows[r] == 0) continue;
+      FRM_HIP(ctx, hipSetDevice(member(ctx, r)->device));
+      FRM_HIP(ctx, hipEventRecord(G.comm_done[r], st[r]));
+      if (r > 0) FRM_HIP(ctx, hipEventRecord(gs.sent[r], st[r]));
+    }
+    G.comm_pending = true;
+  } else {
+    for (uint32_t r = 1; r < n; ++r) {
+      const size_t bytes = (size_t)rows[r] * ctx->width * 4u;
+      if (!bytes) continue;
+      FRM_HIP(ctx, hipSetDevice(G.sub[r]->device));
+      FRM_HIP(ctx, hipEventRecord(gs.rendered[r], st[r]));
+      FRM_HIP(ctx, hipSetDevice(ctx->device));
+      FRM_HIP(ctx, hipStreamWaitEvent(s0, gs.rendered[r], 0));
+      FRM_HIP(ctx, hipMemcpyAsync(gs.gathered + (size_t)r * G.stride, gs.bands[r], bytes, hipMemcpyDeviceToDevice, s0));
+    }
+    FRM_HIP(ctx, hipSetDevice(ctx->device));
+    FRM_HIP(ctx, hipEventRecord(gs.copied, s0));
+  }
+  gs.gather_pending = true;
+  // reassemble; the slot's `done` now covers render, gather and reassembly
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  FRM_HIP(ctx, launch_unshuffle(gs.gathered, G.stride, sl.fb, ctx->width, ctx->height, G.band_rows, n, s0));
+  FRM_HIP(ctx, hipEventRecord(sl.done, s0));
+  ctx->last_slot = si;
+  ctx->render_seq = sl.seq;
+  ctx->render_params = ctx->params;
+  ctx->render_scene = ctx->scene;
+  if (stats) {
+    FRM_HIP(ctx, hipEventRecord(ctx->ev_stop, s0));
+    uint64_t sum[FRM_NUM_COUNTERS] = {};
+    for (uint32_t r = 0; r < n; ++r) {
+      if (r > 0 && rows[r] == 0) continue;
+      frm_ctx* c = member(ctx, r);
+      uint64_t host[FRM_NUM_COUNTERS];
+      FRM_HIP(ctx, hipSetDevice(c->device));
+      FRM_HIP(ctx, hipMemcpyAsync(host, c->counters, sizeof(host), hipMemcpyDeviceToHost, st[r]));
+      FRM_HIP(ctx, hipStreamSynchronize(st[r]));
+      for (uint32_t k = 0; k < FRM_NUM_COUNTERS; ++k) sum[k] += host[k];
+    }
+    FRM_HIP(ctx, hipSetDevice(ctx->device));
+    FRM_HIP(ctx, hipStreamSynchronize(s0));
+    float ms = 0.0f;
+    FRM_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
+    if ((rc = frm_stats_from_counters(ctx, sum, stats))) return rc;
+    stats->kernel_ms = ms;  // device 0's view: from its render's start to the reassembled frame
+  }
+  return FRM_OK;
+}
+
+int group_synchronize(frm_ctx* ctx) {
+  for (uint32_t r = 1; r < ctx->group->n; ++r) {
+    frm_ctx* c = ctx->group->sub[r];
+    FRM_HIP(ctx, hipSetDevice(c->device));
+    if (int rc = synchronize_all(c)) return relay(ctx, c, rc);
+  }
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  return synchronize_all(ctx);
+}
+
 }  // namespace
 
 extern "C" {
@@ -460,6 +663,10 @@ int frm_device_count(int32_t* out_count) {
   return FRM_OK;
 }
 
+// One single-device context on `device` (frm_create's checks done).
+static int create_one(const frm_config* config, int device, frm_ctx** out_ctx);
+static int create_group(const frm_config* config, frm_ctx** out_ctx);
+
 int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   if (!out_ctx || !config) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "out_ctx/config is NULL");
   *out_ctx = nullptr;
@@ -474,15 +681,29 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
       (config->flags & kernels) == kernels)
     return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.flags 0x%x: unknown flag or both kernel flags",
                 config->flags);
+  if (config->device_count > FRM_MAX_DEVICES)
+    return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "config.device_count %u above %u", config->device_count,
+                FRM_MAX_DEVICES);
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n == 0)
     return fail(nullptr, FRM_ERR_NO_DEVICE, "no HIP device available (%s)", hipGetErrorString(e));
-  if (config->device < 0 || config->device >= n)
-    return fail(nullptr, FRM_ERR_NO_DEVICE, "device %d out of range [0, %d)", config->device, n);
+  if (config->device_count == 0) {
+    if (config->device < 0 || config->device >= n)
+      return fail(nullptr, FRM_ERR_NO_DEVICE, "device %d out of range [0, %d)", config->device, n);
+    return create_one(config, config->device, out_ctx);
+  }
+  for (uint32_t r = 0; r < config->device_count; ++r)
+    if (config->devices[r] < 0 || config->devices[r] >= n)
+      return fail(nullptr, FRM_ERR_NO_DEVICE, "devices[%u] = %d out of range [0, %d)", r, config->devices[r], n);
+  return create_group(config, out_ctx);
+}
+
+static int create_one(const frm_config* config, int device, frm_ctx** out_ctx) {
+  hipError_t e = hipSuccess;
   frm_ctx* ctx = new (std::nothrow) frm_ctx();
   if (!ctx) return fail(nullptr, FRM_ERR_OUT_OF_MEMORY, "host allocation failed");
-  ctx->device = config->device;
+  ctx->device = device;
   ctx->max_steps = config->max_steps ? config->max_steps : FRM_DEFAULT_MAX_STEPS;
   ctx->flags = config->flags;
   ctx->nslots = config->frames_in_flight ? config->frames_in_flight : 1u;
@@ -537,8 +758,100 @@ int frm_create(frm_ctx** out_ctx, const frm_config* config) {
   return FRM_OK;
 }
 
+// A group: the context on devices[0] plus one band-rendering context per further device, the
+// RCCL communicator over them (ncclCommInitAll: one process, one rank per device) when the
+// devices are distinct, and the per-slot gather events.
+static int create_group(const frm_config* config, frm_ctx** out_ctx) {
+  const uint32_t n = config->device_count;
+  frm_ctx* ctx = nullptr;
+  int rc = create_one(config, config->devices[0], &ctx);
+  if (rc) return rc;
+  Group* G = new (std::nothrow) Group();
+  if (!G) {
+    frm_destroy(ctx);
+    return fail(nullptr, FRM_ERR_OUT_OF_MEMORY, "host allocation failed");
+  }
+  ctx->group = G;
+  G->n = n;
+  bool distinct = true;
+  for (uint32_t r = 0; r < n; ++r)
+    for (uint32_t q = 0; q < r; ++q) distinct = distinct && config->devices[q] != config->devices[r];
+  const char* gather = getenv("FRM_GATHER");  // experiments: "copy" = device-to-device copies
+  G->rccl = n > 1 && distinct && !(gather && strcmp(gather, "copy") == 0);
+  hipError_t e = hipSuccess;
+  for (uint32_t r = 1; r < n && rc == FRM_OK; ++r) {
+    if ((rc = create_one(config, config->devices[r], &G->sub[r]))) break;
+    G->sub[r]->bands_only = true;
+  }
+  for (uint32_t r = 0; r < n && rc == FRM_OK; ++r) {
+    const int dev = config->devices[r];
+    if ((e = hipSetDevice(dev)) != hipSuccess) { rc = hip_fail(ctx, e, "hipSetDevice"); break; }
+    if ((e = hipEventCreateWithFlags(&G->comm_done[r], hipEventDisableTiming)) != hipSuccess) {
+      rc = hip_fail(ctx, e, "hipEventCreate");
+      break;
+    }
+    for (uint32_t i = 0; i < ctx->nslots && rc == FRM_OK; ++i) {
+      GroupSlot& gs = G->slots[i];
+      if (r == 0) {
+        if ((e = hipEventCreateWithFlags(&gs.copied, hipEventDisableTiming)) != hipSuccess) rc = hip_fail(ctx, e, "hipEventCreate");
+      } else if ((e = hipEventCreateWithFlags(&gs.sent[r], hipEventDisableTiming)) != hipSuccess ||
+                 (e = hipEventCreateWithFlags(&gs.rendered[r], hipEventDisableTiming)) != hipSuccess) {
+        rc = hip_fail(ctx, e, "hipEventCreate");
+      }
+    }
+  }
+  if (rc == FRM_OK && G->rccl) {
+    int devs[FRM_MAX_DEVICES];
+    for (uint32_t r = 0; r < n; ++r) devs[r] = config->devices[r];
+    const ncclResult_t nr = ncclCommInitAll(G->comm, (int)n, devs);
+    if (nr != ncclSuccess) {
+      for (uint32_t r = 0; r < n; ++r) G->comm[r] = nullptr;
+      rc = fail(ctx, FRM_ERR_HIP, "ncclCommInitAll over %u devices failed: %s", n, ncclGetErrorString(nr));
+    }
+  }
+  if (rc == FRM_OK) {
+    e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) rc = hip_fail(ctx, e, "hipSetDevice");
+  }
+  if (rc != FRM_OK) {
+    g_error = ctx->error;
+    frm_destroy(ctx);
+    return rc;
+  }
+  *out_ctx = ctx;
+  return FRM_OK;
+}
+
 int frm_destroy(frm_ctx* ctx) {
   if (!ctx) return FRM_OK;
+  if (Group* G = ctx->group) {  // the members first (best effort, statuses ignored)
+    for (uint32_t r = 1; r < G->n; ++r) {
+      frm_ctx* c = G->sub[r];
+      if (!c) continue;
+      (void)hipSetDevice(c->device);
+      (void)synchronize_all(c);
+      for (uint32_t i = 0; i < FRM_MAX_FRAMES_IN_FLIGHT; ++i) {
+        GroupSlot& gs = G->slots[i];
+        if (gs.bands[r] && c->stream) (void)hipFreeAsync(gs.bands[r], c->stream);
+        for (hipEvent_t ev : {gs.sent[r], gs.rendered[r]})
+          if (ev) (void)hipEventDestroy(ev);
+      }
+      if (G->comm_done[r]) (void)hipEventDestroy(G->comm_done[r]);
+      if (G->comm[r]) (void)ncclCommDestroy(G->comm[r]);
+      frm_destroy(c);
+    }
+    (void)hipSetDevice(ctx->device);
+    (void)synchronize_all(ctx);
+    for (uint32_t i = 0; i < FRM_MAX_FRAMES_IN_FLIGHT; ++i) {
+      GroupSlot& gs = G->slots[i];
+      if (gs.gathered && ctx->stream) (void)hipFreeAsync(gs.gathered, ctx->stream);
+      if (gs.copied) (void)hipEventDestroy(gs.copied);
+    }
+    if (G->comm_done[0]) (void)hipEventDestroy(G->comm_done[0]);
+    if (G->comm[0]) (void)ncclCommDestroy(G->comm[0]);
+    delete G;
+    ctx->group = nullptr;
+  }
   // Teardown is best effort: statuses are ignored so every resource gets released.
   (void)hipSetDevice(ctx->device);
   for (uint32_t i = 0; i < ctx->nslots; ++i) {
@@ -582,6 +895,17 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
   if (width == 0 || height == 0 || width > FRM_MAX_DIMENSION || height > FRM_MAX_DIMENSION)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "frame size %ux%u outside [1, %u]^2", width, height,
                 FRM_MAX_DIMENSION);
+  if (Group* G = ctx->group) {  // every member follows; the band geometry of the new size
+    for (uint32_t r = 1; r < G->n; ++r)
+      if (int rc = frm_resize(G->sub[r], width, height)) return relay(ctx, G->sub[r], rc);
+    G->band_rows = group_band_rows(height, G->n);
+    G->stride = (size_t)band_local_rows(height, G->band_rows, 0, G->n) * width * 4u;
+  }
+  if (ctx->bands_only) {  // a group member: its band buffers belong to the group's frame slots
+    ctx->width = width;
+    ctx->height = height;
+    return FRM_OK;
+  }
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->slots[0].fb && width == ctx->width && height == ctx->height) return FRM_OK;
   if (!ctx->slots[0].stream) return fail(ctx, FRM_ERR_HIP, "context stream missing");
@@ -595,6 +919,9 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
   ctx->width = width;
   ctx->height = height;
   ctx->last_slot = 0;
+  // no frame of the new size yet: frm_read_frame_async / frm_present_async refuse until the next
+  // frm_render (tickets issued before keep their frames)
+  ctx->render_seq = 0;
   return FRM_OK;
 }
 
@@ -607,12 +934,19 @@ int frm_set_parameters(frm_ctx* ctx, const frm_parameters* parameters) {
   ctx->params = *parameters;
   ctx->scene = su;
   ctx->has_params = true;
+  if (Group* G = ctx->group)  // the members render the same frame (same flags, same uniforms)
+    for (uint32_t r = 1; r < G->n; ++r) {
+      G->sub[r]->params = *parameters;
+      G->sub[r]->scene = su;
+      G->sub[r]->has_params = true;
+    }
   return FRM_OK;
 }
 
 int frm_render(frm_ctx* ctx, frm_stats* stats) {
   int rc = ensure_ready(ctx);
   if (rc) return rc;
+  if (ctx->group) return group_render(ctx, stats);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   if (stats && (rc = synchronize_all(ctx))) return rc;  // the counters must hold this frame alone
   const uint32_t si = ctx->next_slot;
@@ -776,22 +1110,33 @@ int frm_frame_pixels(frm_ctx* ctx, uint64_t ticket, const uint8_t** out_pixels, 
 
 int frm_reload(frm_ctx* ctx, const char* source_dir) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
-  FRM_HIP(ctx, hipSetDevice(ctx->device));
-  ReloadedKernels* rk = nullptr;
-  if (source_dir) {
-    std::string log;
-    const int rc = compile_reloaded(source_dir, ctx->device, &rk, &log);
-    if (rc != FRM_OK) return fail(ctx, rc, "reload failed, previous kernels kept: %s", log.c_str());
+  // a group reloads every member: all compile, or every member keeps its kernels
+  const uint32_t n = ctx->group ? ctx->group->n : 1u;
+  ReloadedKernels* rk[FRM_MAX_DEVICES] = {};
+  if (source_dir)
+    for (uint32_t r = 0; r < n; ++r) {
+      std::string log;
+      const int rc = compile_reloaded(source_dir, member(ctx, r)->device, &rk[r], &log);
+      if (rc != FRM_OK) {
+        for (uint32_t q = 0; q < r; ++q) unload_reloaded(rk[q]);
+        return fail(ctx, rc, "reload failed, previous kernels kept: %s", log.c_str());
+      }
+    }
+  for (uint32_t r = 0; r < n; ++r) {
+    frm_ctx* c = member(ctx, r);
+    // the old module may still run, on this context's stream or a caller's (frm_render_bands)
+    FRM_HIP(ctx, hipSetDevice(c->device));
+    FRM_HIP(ctx, hipDeviceSynchronize());
+    unload_reloaded(c->reloaded);
+    c->reloaded = rk[r];
   }
-  // the old module may still run, on this context's stream or a caller's (frm_render_bands)
-  FRM_HIP(ctx, hipDeviceSynchronize());
-  unload_reloaded(ctx->reloaded);
-  ctx->reloaded = rk;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
   return FRM_OK;
 }
 
 int frm_synchronize(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (ctx->group) return group_synchronize(ctx);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
   return synchronize_all(ctx);
 }
@@ -799,6 +1144,13 @@ int frm_synchronize(frm_ctx* ctx) {
 int frm_kernel_for_pixels(const frm_ctx* ctx, uint64_t pixels, uint32_t* out_kernel) {
   if (!ctx || !out_kernel) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx/out_kernel is NULL");
   *out_kernel = kernel_for(ctx, pixels) == kKernelSimple ? FRM_KERNEL_SIMPLE : FRM_KERNEL_PERSISTENT;
+  return FRM_OK;
+}
+
+int frm_group_band_rows(uint32_t height, uint32_t devices, uint32_t* out_band_rows) {
+  if (!out_band_rows || height == 0 || devices == 0 || devices > FRM_MAX_DEVICES)
+    return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "invalid height %u or device count %u", height, devices);
+  *out_band_rows = group_band_rows(height, devices);
   return FRM_OK;
 }
 
@@ -814,6 +1166,7 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
                      uint32_t first_band, uint32_t band_stride, void* stream, uint64_t* dev_counters) {
   int rc = ensure_ready(ctx);
   if (rc) return rc;
+  if (ctx->group) return not_on_group(ctx, "frm_render_bands");
   if (!dev_dst || band_rows == 0 || band_stride == 0)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "invalid dst or band geometry");
   uint32_t rows = band_local_rows(ctx->height, band_rows, first_band, band_stride);
@@ -832,6 +1185,7 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
                            uint32_t band_stride,
                            void* stream, uint64_t* dev_counters) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (ctx->group) return not_on_group(ctx, "frm_render_bands_batch");
   if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
   if (!params || !dev_dst || count == 0 || count > FRM_MAX_BATCH || band_rows == 0 || band_stride == 0)
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "invalid batch (count %u, at most %u) or band geometry", count,
@@ -942,6 +1296,7 @@ extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
 // the next launch overwrites them)
 int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
   if (!ctx || !out) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (ctx->group) return not_on_group(ctx, "frm_debug_pixel_keys");
   const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
   if (!sl.sched_keys) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "no persistent launch yet");
   if (n > sl.sched_cap) n = sl.sched_cap;
@@ -955,6 +1310,7 @@ int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
 // slot of the next launch must hold the history of a whole frame of the current size
 int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
   if (!ctx || !keys) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (ctx->group) return not_on_group(ctx, "frm_debug_set_pixel_keys");
   Slot& sl = ctx->slots[ctx->next_slot];
   if (!sl.sched_history || !sl.sched_whole || sl.sched_w != ctx->width || sl.sched_h != ctx->height ||
       n != (size_t)ctx->width * ctx->height || n > sl.sched_cap)
@@ -973,6 +1329,7 @@ int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
 int frm_debug_trace(frm_ctx* ctx, float* out, size_t n_floats) {
   int rc = ensure_ready(ctx);
   if (rc) return rc;
+  if (ctx->group) return not_on_group(ctx, "frm_debug_trace");
   if (!out) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "out is NULL");
   const size_t npix = (size_t)ctx->width * ctx->height;
   if (n_floats < npix * 10u)

@@ -7,11 +7,11 @@
 // Where the savings come from (hipcc's correctly rounded lowerings, gfx950):
 //  * sqrt: v_sqrt_f32 + a one-ulp correction; the exact lowering also rescales inputs
 //    below 2^-96 (5 instructions) — not needed when x == 0 or x >= 2^-96.
-//  * a / b: the same Newton sequence as the exact lowering, without v_div_scale (returns
-//    its input unchanged when no operand or quotient is near the exponent limits),
-//    v_div_fmas (a plain fma when v_div_scale did not scale) and v_div_fixup (for
-//    finite non-zero operands with a normal quotient it only re-applies the sign).
-//    Zero numerators are handled exactly: 0 / b = +-0 with sign(a) ^ sign(b).
+//  * 1 / b: v_rcp_f32 + one Newton step is RN(1 / b) for every |b| in [2^-125, 2^125]
+//    (checked over all 4.2 G such encodings on gfx950, tools/micro/hw_exact_probe.hip,
+//    profiles/round5/hw_exact.json): the correctly rounded reciprocal in three instructions.
+//  * a / b: a * RN(1 / b) corrected once (Markstein), in place of LLVM's division sequence
+//    (v_div_scale, v_rcp, Newton steps, v_div_fmas, v_div_fixup).
 //  * log2 / exp2: the special-value selects are dead for positive normal finite inputs /
 //    finite exponents; the exponent split of log2 and the scaling of exp2 are integer
 //    arithmetic on the encodings where the operand (log2) / result (exp2) is normal.
@@ -36,32 +36,30 @@ __device__ __forceinline__ float sqrt_nosmall(float x) {
   return (r_up > 0.0f) ? s_up : s;
 }
 
-// Correctly rounded a / b for a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40].
-__device__ __forceinline__ float div_tame(float a, float b) {
-  float r = __builtin_amdgcn_rcpf(b);
-  float e = fmaf(-b, r, 1.0f);
-  r = fmaf(e, r, r);
-  float q = a * r;
-  float rem = fmaf(-b, q, a);
-  q = fmaf(rem, r, q);
-  rem = fmaf(-b, q, a);
-  q = fmaf(rem, r, q);
-  const float zero = __uint_as_float((__float_as_uint(a) ^ __float_as_uint(b)) & 0x80000000u);
-  return (a == 0.0f) ? zero : q;
+// RN(1 / b) for |b| in [2^-125, 2^125] (exhaustively checked, see above).
+__device__ __forceinline__ float rcp_rn(float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  return fmaf(fmaf(-b, r, 1.0f), r, r);
 }
 
-// div_tame without the zero-numerator fix-up: for a = +0 the Newton sequence already
-// gives +0; for a = -0 it gives +0 where a / b is -0. Used where that sign cannot matter
-// (acos_dev(+-0) and atan2's min/max ratio, whose numerator is never -0).
+// Correctly rounded a / b for a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40]: from the
+// correctly rounded reciprocal y = RN(1/b), q = RN(a y) is within one ulp of a / b and one
+// Markstein correction RN(q + RN(a - b q) y) (the remainder is exact) is RN(a / b)
+// (Markstein's theorem; no operand, quotient or remainder near the exponent limits here).
+// Zero numerators are handled exactly: 0 / b = +-0 with sign(a) ^ sign(b).
+__device__ __forceinline__ float div_tame(float a, float b) {
+  const float y = rcp_rn(b);
+  const float q = a * y;
+  const float r = fmaf(fmaf(-b, q, a), y, q);
+  return (a == 0.0f) ? q : r;
+}
+
+// div_tame without the zero-numerator fix-up: for a = -0 the correction gives +0 where a / b
+// is -0. Used where that sign cannot matter (acos_dev(+-0)).
 __device__ __forceinline__ float div_tame_nz(float a, float b) {
-  float r = __builtin_amdgcn_rcpf(b);
-  float e = fmaf(-b, r, 1.0f);
-  r = fmaf(e, r, r);
-  float q = a * r;
-  float rem = fmaf(-b, q, a);
-  q = fmaf(rem, r, q);
-  rem = fmaf(-b, q, a);
-  return fmaf(rem, r, q);
+  const float y = rcp_rn(b);
+  const float q = a * y;
+  return fmaf(fmaf(-b, q, a), y, q);
 }
 
 // max_(a, b) for operands that are never signalling NaNs (values computed here): plain v_max_f32,
@@ -72,29 +70,14 @@ __device__ __forceinline__ float max_quiet(float a, float b) {
   return r;
 }
 
-// a / b from a precomputed reciprocal r within one ulp of 1 / b: div_tame's two Newton
-// corrections (the same domain: a in {+-0} U +-[2^-60, 2^40], b in +-[2^-60, 2^40]), with the
-// sign of a zero quotient restored; b > 0 here (the Menger scales), so 0 / b keeps a's sign.
-__device__ __forceinline__ float div_by_rcp(float a, float b, float r) {
-  float q = a * r;
-  float rem = fmaf(-b, q, a);
-  q = fmaf(rem, r, q);
-  rem = fmaf(-b, q, a);
-  q = fmaf(rem, r, q);
-  return (a == 0.0f) ? a : q;
+// a / b from the precomputed y = RN(1 / b) (b > 0, the Menger scales; a in {+-0} U
+// +-[2^-60, 2^40]): div_tame's correction, with the sign of a zero quotient kept (0 / b = a).
+__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
+  const float q = a * y;
+  const float r = fmaf(fmaf(-b, q, a), y, q);
+  return (a == 0.0f) ? a : r;
 }
 
-// sincos_ for finite |x| <= 2^22 * pi/2 (the quadrant clamp is a no-op there); negating through
-// the sign bit: (q & 2) ? -v : v == v ^ (bit 1 of q moved to bit 31). Bit-identical.
-// rint(x * 2/pi) by the 1.5 * 2^23 rounding constant: |x * 2/pi| < 2^22, so t = x * 2/pi + K
-// rounds to an integer (to nearest even, as rint does), j = t - K is exact and the low bits
-// of t's encoding are j mod 2^22 (two v_add in place of v_rndne + v_cvt). The odd-quadrant
-// swap is a bit-field select on a sign-extended bit 0 (no compare, no v_cndmask).
-__device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) {  // (mask & a) | (~mask & b)
-  uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
-  return r;
-}
 // v ^ (m & 0x80000000) in one v_bitop3_b32 (truth table 0x6c: (src0 & src2) ^ src1); left to
 // itself the compiler sometimes splits it into v_and + v_xor
 __device__ __forceinline__ uint32_t xor_sign_(uint32_t v, uint32_t m) {
@@ -106,46 +89,42 @@ __device__ __forceinline__ uint32_t xor_sign_(uint32_t v, uint32_t m) {
   return v ^ (m & 0x80000000u);
 #endif
 }
-__device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
-  const float tq = x * kTwoOverPi + 0x1.8p23f;
-  const float j = tq - 0x1.8p23f;
-  const uint32_t q = __float_as_uint(tq);
-  float r = fma_(-j, kHalfPi, x);
-  r = fma_(-j, kHalfPiLo, r);
-  float z = r * r;
-  float ps = fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
-  float s = fma_(r * z, ps, r);
-  float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
-                  4.166664568298827e-2f);
-  float c = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
-  const uint32_t odd = (uint32_t)((int32_t)(q << 31) >> 31);  // v_bfe_i32 q, 0, 1
-  const float sv = __uint_as_float(bfi_(odd, __float_as_uint(c), __float_as_uint(s)));
-  const float cv = __uint_as_float(bfi_(odd, __float_as_uint(s), __float_as_uint(c)));
-  *s_out = __uint_as_float(xor_sign_(__float_as_uint(sv), q << 30));
-  *c_out = __uint_as_float(xor_sign_(__float_as_uint(cv), (q + 1u) << 30));
+__device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) {  // (mask & a) | (~mask & b)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+  return r;
 }
 
-// acos_ with the exact-for-its-range sqrt (zb is 0 or >= 2^-25 for |t| <= 1; NaN/negative
-// inputs propagate NaN exactly as sqrtf does).
+// sincos_ for |x| <= 2^20 (the branch sincos_ takes there): t = fma(x, 1/pi, K), j = t - K,
+// and j's parity is t's low bit, so the sign (-1)^j of both results is bit 0 of t moved to
+// bit 31 (returned in *sign_out: the caller applies it, sincos_small applies it itself).
+__device__ __forceinline__ void sincos_unsigned(float x, float* s_out, float* c_out, uint32_t* sign_out) {
+  const float t = fma_(x, kInvPiHi, kRoundK);
+  const float j = t - kRoundK;
+  float r = fma_(x, kInvPiHi, -j);
+  r = fma_(x, kInvPiLo, r);
+  const float u = r * r;
+  *s_out = r * sinpi_poly(u);
+  *c_out = cospi_poly(u);
+  *sign_out = __float_as_uint(t) << 31;
+}
+__device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
+  float s, c;
+  uint32_t sg;
+  sincos_unsigned(x, &s, &c, &sg);
+  *s_out = __uint_as_float(__float_as_uint(s) ^ sg);
+  *c_out = __uint_as_float(__float_as_uint(c) ^ sg);
+}
+
+// acos_ with the exact-for-its-range sqrt (1 - |t| is 0 or >= 2^-24 for |t| <= 1; NaN/negative
+// inputs propagate NaN exactly as sqrtf does). The t < 0 branch pi - r as fma(r, sg, off) with
+// sg = t < 0 ? -1 : 1 (t's sign bit) and off = fma(sg, -pi/2, pi/2) in {+0, pi}: one rounding
+// either way; t = -0 gives pi - pi/2 = pi/2 exactly, the value of the t >= 0 branch.
 __device__ __forceinline__ float acos_dev(float t) {
-  float a = fabsf(t);
-  bool big = a > 0.5f;
-  float zb = 0.5f * (1.0f - a);
-  float z = big ? zb : a * a;
-  float w = big ? sqrt_nosmall(zb) : a;
-  float p = fma_(fma_(fma_(fma_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
-                      7.4953002686e-2f), z, 1.6666752422e-1f);
-  float s = fma_(w * z, p, w);
-  // rb is used only for |t| > 1/2 (t != 0): t > 0 is t's sign bit, and (t > 0 ? 2s : pi - 2s)
-  // == fma(2s, t < 0 ? -1 : 1, t < 0 ? pi : 0), one rounding either way
-  const uint32_t tb = __float_as_uint(t);
-  const float sg = __uint_as_float(bfi_(0x80000000u, tb, 0x3f800000u));  // t < 0 ? -1 : 1
-  // the offset (t < 0 ? pi : 0) as fma(sg, -pi/2, pi/2): exact (+0 or pi), one FMA-class
-  // instruction instead of a shift and a mask
-  float rb = fma_(2.0f * s, sg, fma_(sg, -0.5f * kPi, 0.5f * kPi));
-  // pi/2 - copysign(s, t) == fma(-sg, s, pi/2): sg * s is exact (+-s; t = -0 gives sg = -1)
-  float rs = fma_(-sg, s, kHalfPi);
-  return big ? rb : rs;
+  const float a = fabsf(t);
+  const float r = sqrt_nosmall(1.0f - a) * acos_poly(a);
+  const float sg = __uint_as_float(bfi_(0x80000000u, __float_as_uint(t), 0x3f800000u));
+  return fma_(r, sg, fma_(sg, -0.5f * kPi, 0.5f * kPi));
 }
 
 // atan2_ for tame x, y (each 0 or with magnitude in [2^-60, 2^40]).
@@ -155,17 +134,13 @@ __device__ __forceinline__ float atan2_tame(float y, float x) {
   // |.| source modifiers, without the NaN-quieting canonicalizes the compiler adds to
   // fmaxf / fminf in IEEE mode (same values for non-NaN operands). Tame non-zero
   // magnitudes are >= 2^-60, so the 2^-100 floor only replaces mx = 0 (x = y = 0), where
-  // the Newton division then gives 0 / 2^-100 = +0: the value atan2's a = 0 branch needs.
+  // a = 0 * RN(2^100) = +0: the value atan2's mx = 0 branch sets.
   float mx, mn;
   asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(mx) : "v"(x), "v"(y), "s"(0x1p-100f));
   asm("v_min_f32 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
-  const float a = div_tame_nz(mn, mx);  // mn >= +0
-  float s = a * a;
-  float q = fma_(fma_(fma_(fma_(fma_(fma_(fma_(0.002974590389872539f, s, -0.016581183968493302f), s,
-                                      0.04355353931255974f), s, -0.07580578130128461f), s,
-                          0.10678940285181907f), s, -0.14214209135918496f), s,
-                0.1999413720560495f), s, -0.3333316696611865f);
-  float r = fma_(a * s, q, a);
+  const float a = mn * rcp_rn(mx);
+  const float s = a * a;
+  float r = fma_(a * s, atan_poly(s), a);
   // the octant fix-ups without compares: (c ? h - r : r) == fma(r, c ? -1 : 1, c ? h : 0), one
   // rounding either way (r >= +0); the +-1 is a bit-field insert of c's sign bit into 1.0.
   // c = sign bit of ax - ay (exact difference: negative iff ay > ax, +0 when equal) and of
@@ -194,15 +169,14 @@ __device__ __forceinline__ void log_split_normal(float x, float* f_out, float* e
 __device__ __forceinline__ float log2_tame(float x) {
   float f, fe;
   log_split_normal(x, &f, &fe);
-  return fma_(log1p_kernel_(f), kLog2e, fe);
+  return fma_(f, log2_poly(f), fe);
 }
 
 // log_ for positive normal finite x (log_posfinite_ with the integer split).
 __device__ __forceinline__ float log_posnormal(float x) {
   float f, fe;
   log_split_normal(x, &f, &fe);
-  float l = log1p_kernel_(f);
-  return fma_(fe, 0.693359375f, fma_(fe, -2.12194440e-4f, l));
+  return ln_from_split_(f, fe);
 }
 
 // exp2_ for finite y whose rint lies in [-125, 127] (y in [-125.5, 127.5)): there the
@@ -212,13 +186,10 @@ __device__ __forceinline__ float log_posnormal(float x) {
 // (one v_lshl_add_u32 in place of v_rndne, v_cvt and v_ldexp). The clamp to [-151, 129]
 // cannot fire there.
 __device__ __forceinline__ float exp2_tame(float y) {
-  const float t = y + 0x1.8p23f;
-  const float k = t - 0x1.8p23f;
-  float f = y - k;
-  float p = fma_(fma_(fma_(fma_(fma_(1.535336188319500e-4f, f, 1.339887440266574e-3f), f,
-                               9.618437357674640e-3f), f, 5.550332471162809e-2f), f,
-                     2.402264791363012e-1f), f, 6.931472028550421e-1f);
-  return __uint_as_float(__float_as_uint(fma_(f, p, 1.0f)) + (__float_as_uint(t) << 23));
+  const float t = y + kRoundK;
+  const float k = t - kRoundK;
+  const float f = y - k;
+  return __uint_as_float(__float_as_uint(fma_(f, exp2_poly(f), 1.0f)) + (__float_as_uint(t) << 23));
 }
 
 #endif  // __HIP_DEVICE_COMPILE__

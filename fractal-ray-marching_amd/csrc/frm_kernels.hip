@@ -164,15 +164,23 @@ static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStre
 template <uint32_t FAM, bool ITERS>
 static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStream_t stream,
                                     const ReloadedKernels* rk) {
-  static int blocks_per_cu = 0;  // occupancy of this instantiation (per process)
+  // occupancy of each built-in instantiation (per process); reloaded modules query their own
+  // (frm_reload.hip)
+  static int blocks_per_cu = 0, blocks_per_cu_anim = 0;
   if (blocks_per_cu == 0) {
     int n = 0;
     hipError_t e =
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS, true>, kMarchBlock, 0);
     if (e != hipSuccess) return e;
     blocks_per_cu = n > 0 ? n : 1;
+    blocks_per_cu_anim = blocks_per_cu;
+    if constexpr (is_mandelbulb(FAM) && ITERS) {
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS, true, true>, kMarchBlock, 0);
+      if (e != hipSuccess) return e;
+      blocks_per_cu_anim = n > 0 ? n : 1;
+    }
   }
-  int bpc = rk ? rk->persistent_blocks_per_cu[FAM][ITERS] : blocks_per_cu;
+  int bpc = rk ? rk->persistent_blocks_per_cu[FAM][ITERS] : (args.anim ? blocks_per_cu_anim : blocks_per_cu);
   if (const int v = blocks_override()) bpc = v;
   // every wave starts with one chunk of 64 pixels; never launch more waves than chunks
   uint32_t blocks = (uint32_t)(bpc * cu_count);

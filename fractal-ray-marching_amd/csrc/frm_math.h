@@ -10,10 +10,11 @@
 // minNum/maxNum, comparisons and selects. No hardware transcendental instruction
 // (v_sin/v_cos/v_exp/v_log/v_rcp/v_rsq) ever contributes to a result bit.
 //
-// The polynomial kernels and their constants are specified in DESIGN.md §"frm math";
-// oracle/frm_oracle.c restates them independently for the CPU. Accuracy (measured by
-// tests/test_oracle_math.py against float64 libm): sin/cos/acos/atan2/log/log2/exp2
-// within a few f32 ulp on the ranges the path uses — tighter than WGSL requires.
+// frm semantics v2 (round 5): the polynomial kernels and their constants are specified in
+// DESIGN.md section 2 (fitted by tools/v2fit.py); oracle/frm_oracle.c restates them
+// independently for the CPU. Accuracy (tests/test_oracle_math.py, against float64 libm):
+// sin/cos/acos/atan2/log/log2/exp2 within a few f32 ulp on the ranges the path uses —
+// tighter than WGSL requires.
 //
 // Compile with -ffp-contract=off on both host and device: every fusion below is an
 // explicit fma.
@@ -38,9 +39,9 @@ namespace frm {
 // ---- constants (WGSL abstract-float constants rounded once to f32) -------------
 constexpr float kPi = 3.14159274101257324219f;         // f32(pi)
 constexpr float kHalfPi = 1.57079637050628662109f;     // f32(pi/2)
-constexpr float kHalfPiLo = -4.37113900018624283e-8f;  // f32(pi/2 - f32(pi/2))
-constexpr float kTwoOverPi = 0.636619746685028076172f; // f32(2/pi)
-constexpr float kLog2e = 1.44269502162933349609f;      // f32(log2(e))
+constexpr float kInvPiHi = 0x1.45f306p-2f;             // f32(1/pi)
+constexpr float kInvPiLo = 0x1.b93910p-27f;            // f32(1/pi - kInvPiHi)
+constexpr float kRoundK = 0x1.8p23f;                   // 1.5 * 2^23: x + K rounds x to an integer
 constexpr float kSqrtHalf = 0.707106769084930419922f;  // f32(sqrt(1/2))
 constexpr float kInf = __builtin_huge_valf();
 
@@ -53,62 +54,91 @@ FRM_HD float fract_(float x) { return x - floorf(x); }       // WGSL fract(e) = 
 FRM_HD float clamp_(float x, float lo, float hi) { return min_(max_(x, lo), hi); }
 // WGSL mix(e1,e2,e3) = e1*(1-e3) + e2*e3: two products and an add, no fusion.
 FRM_HD float mix_(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+FRM_HD uint32_t bits_(float x) { uint32_t u; __builtin_memcpy(&u, &x, 4); return u; }
+
+// ---- frm semantics v2 polynomial kernels (minimax fits, tools/v2fit.py) ------------
+// Horner with fma, lowest-order coefficient first in the name: c0 + x (c1 + x (c2 + ...)).
+// sin(pi r) / r and cos(pi r) in u = r^2, r in [-1/2, 1/2]
+FRM_HD float sinpi_poly(float u) {
+  return fma_(fma_(fma_(fma_(0x1.3daffap-4f, u, -0x1.324cccp-1f), u, 0x1.4668b0p+1f), u, -0x1.4abbc2p+2f), u,
+              0x1.921fb6p+1f);
+}
+FRM_HD float cospi_poly(float u) {
+  return fma_(fma_(fma_(fma_(0x1.c2b9aap-3f, u, -0x1.55041ap+0f), u, 0x1.03bdaap+2f), u, -0x1.3bd3b0p+2f), u, 1.0f);
+}
+// acos(a) / sqrt(1 - a), a in [0, 1], with P(0) = f32(pi/2)
+FRM_HD float acos_poly(float a) {
+  return fma_(fma_(fma_(fma_(fma_(fma_(0x1.35deb4p-9f, a, -0x1.748422p-7f), a, 0x1.bd48d6p-6f), a, -0x1.912814p-5f),
+                        a, 0x1.6bbdc6p-4f), a, -0x1.b77b98p-3f), a, 0x1.921fb6p+0f);
+}
+// (atan(a) - a) / a^3 in s = a^2, a in [0, 1]
+FRM_HD float atan_poly(float s) {
+  return fma_(fma_(fma_(fma_(fma_(fma_(-0x1.3c0c38p-8f, s, 0x1.953dcap-6f), s, -0x1.ed2edep-5f), s, 0x1.984ef0p-4f),
+                        s, -0x1.1f90fcp-3f), s, 0x1.991268p-3f), s, -0x1.5552dep-2f);
+}
+// log2(1 + f) / f and ln(1 + f) / f, f in [sqrt(1/2) - 1, sqrt(2) - 1]
+FRM_HD float log2_poly(float f) {
+  return fma_(fma_(fma_(fma_(fma_(fma_(fma_(-0x1.2a9f30p-3f, f, 0x1.df5156p-3f), f, -0x1.fdb316p-3f), f,
+                                  0x1.25fd38p-2f), f, -0x1.70e2aap-2f), f, 0x1.ec7724p-2f), f, -0x1.715528p-1f), f,
+              0x1.715476p+0f);
+}
+FRM_HD float ln_poly(float f) {
+  return fma_(fma_(fma_(fma_(fma_(fma_(fma_(-0x1.9dfa4ep-4f, f, 0x1.4c3cdcp-3f), f, -0x1.614bfcp-3f), f,
+                                  0x1.978e32p-3f), f, -0x1.ff623ep-3f), f, 0x1.5559dcp-2f), f, -0x1.00007ap-1f), f,
+              0x1.fffffep-1f);
+}
+// (2^f - 1) / f, f in [-1/2, 1/2]
+FRM_HD float exp2_poly(float f) {
+  return fma_(fma_(fma_(fma_(0x1.5bb9f4p-10f, f, 0x1.3cea80p-7f), f, 0x1.c6b752p-5f), f, 0x1.ebf9bcp-3f), f,
+              0x1.62e42ap-1f);
+}
 
 // ---- sin / cos --------------------------------------------------------------
-// j = rint(x*2/pi); r = x - j*pi/2 (two fma, Cody-Waite); minimax polynomials on
-// [-pi/4, pi/4]; quadrant select. j is clamped to +-2^22 before the int conversion so
-// NaN/inf inputs are well defined (they yield NaN through r).
+// Half-turn reduction: r = x/pi - j, j the nearest integer (|r| <= 1/2, the 1/pi product in
+// two parts); sin x = (-1)^j r S(r^2), cos x = (-1)^j C(r^2). For |x| <= 2^20, j is rint of the
+// exact product x * kInvPiHi, taken from t = fma(x, kInvPiHi, K), whose ulp is 1 (its low bit
+// is j's parity); larger and non-finite x take j = rint(RN(x * kInvPiHi)) (defined but not
+// accurate there: WGSL bounds sin/cos on [-pi, pi] only; NaN and inf give NaN).
 FRM_HD void sincos_(float x, float* s_out, float* c_out) {
-  float j = rintf(x * kTwoOverPi);
-  float r = fma_(-j, kHalfPi, x);
-  r = fma_(-j, kHalfPiLo, r);
-  int q = (int)min_(max_(j, -4194304.0f), 4194304.0f);
-  float z = r * r;
-  float ps = fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
-  float s = fma_(r * z, ps, r);
-  float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
-                  4.166664568298827e-2f);
-  float c = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
-  float sv = (q & 1) ? c : s;
-  float cv = (q & 1) ? s : c;
-  *s_out = (q & 2) ? -sv : sv;
-  *c_out = ((q + 1) & 2) ? -cv : cv;
+  const float t = fma_(x, kInvPiHi, kRoundK);
+  float j;
+  uint32_t odd;
+  if (fabsf(x) <= 0x1p20f) {
+    j = t - kRoundK;
+    odd = bits_(t) & 1u;
+  } else {
+    j = rintf(x * kInvPiHi);
+    odd = fabsf(j) < 0x1p24f ? (uint32_t)((int32_t)j & 1) : 0u;
+  }
+  float r = fma_(x, kInvPiHi, -j);
+  r = fma_(x, kInvPiLo, r);
+  const float u = r * r;
+  const float s = r * sinpi_poly(u);
+  const float c = cospi_poly(u);
+  *s_out = odd ? -s : s;
+  *c_out = odd ? -c : c;
 }
 FRM_HD float sin_(float x) { float s, c; sincos_(x, &s, &c); return s; }
 FRM_HD float cos_(float x) { float s, c; sincos_(x, &s, &c); return c; }
 
 // ---- acos -------------------------------------------------------------------
-// asin kernel on w in [0, 1/2]: asin(w) = w + w*z*P(z); |t| > 1/2 uses
-// w = sqrt((1-|t|)/2), z = w^2 (computed as (1-|t|)/2 directly).
+// acos(t) = sqrt(1 - |t|) P(|t|) for t >= 0 (+-0 included), pi - that for t < 0.
 FRM_HD float acos_(float t) {
-  float a = fabsf(t);
-  bool big = a > 0.5f;
-  float zb = 0.5f * (1.0f - a);
-  float z = big ? zb : a * a;
-  float w = big ? sqrt_(zb) : a;
-  float p = fma_(fma_(fma_(fma_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
-                      7.4953002686e-2f), z, 1.6666752422e-1f);
-  float s = fma_(w * z, p, w);
-  float rb = (t > 0.0f) ? 2.0f * s : kPi - 2.0f * s;
-  float rs = kHalfPi - copysignf(s, t);
-  return big ? rb : rs;
+  const float a = fabsf(t);
+  const float r = sqrt_(1.0f - a) * acos_poly(a);
+  return t < 0.0f ? kPi - r : r;
 }
 
 // ---- atan2 ------------------------------------------------------------------
-// a = min(|x|,|y|)/max(|x|,|y|) in [0,1]; atan(a) = a + a*s*Q(s), s = a^2, Q a degree-7
-// minimax fit (Remez, relative error 1.5e-8 on [0,1]); octant/quadrant fix-up.
-// atan2(+-0, +-0) = +-0 (a := 0).
+// a = min(|x|,|y|) * RN(1 / max(|x|,|y|)) in [0,1] (0 when both are 0); atan(a) = a + a s Q(s),
+// s = a^2; octant/quadrant fix-up. atan2(+-0, +-0) = +-0.
 FRM_HD float atan2_(float y, float x) {
   float ax = fabsf(x), ay = fabsf(y);
   float mx = max_(ax, ay), mn = min_(ax, ay);
-  float a = mn / mx;
+  float a = mn * (1.0f / mx);
   a = (mx == 0.0f) ? 0.0f : a;
   float s = a * a;
-  float q = fma_(fma_(fma_(fma_(fma_(fma_(fma_(0.002974590389872539f, s, -0.016581183968493302f), s,
-                                      0.04355353931255974f), s, -0.07580578130128461f), s,
-                          0.10678940285181907f), s, -0.14214209135918496f), s,
-                0.1999413720560495f), s, -0.3333316696611865f);
-  float r = fma_(a * s, q, a);
+  float r = fma_(a * s, atan_poly(s), a);
   r = (ay > ax) ? kHalfPi - r : r;
   r = (x < 0.0f) ? kPi - r : r;
   return copysignf(r, y);
@@ -116,16 +146,8 @@ FRM_HD float atan2_(float y, float x) {
 
 // ---- log / log2 -------------------------------------------------------------
 // x = m*2^e with m in [sqrt(1/2), sqrt(2)) (frexp + one exact doubling); f = m-1 (exact);
-// ln(1+f) = f - z/2 + f*z*P(f), z = f^2, P degree 8.
+// log2 x = e + f Q(f) (one fma); ln x = e ln2 + f L(f) (ln 2 in two parts).
 // Special values: log(+0/-0) = -inf, log(x<0) = NaN, log(+inf) = +inf, log(NaN) = NaN.
-FRM_HD float log1p_kernel_(float f) {
-  float z = f * f;
-  float p = fma_(fma_(fma_(fma_(fma_(fma_(fma_(fma_(7.0376836292e-2f, f, -1.1514610310e-1f), f,
-        1.1676998740e-1f), f, -1.2420140846e-1f), f, 1.4249322787e-1f), f, -1.6668057665e-1f), f,
-        2.0000714765e-1f), f, -2.4999993993e-1f), f, 3.3333331174e-1f);
-  float y = fma_(-0.5f, z, (f * z) * p);
-  return f + y;
-}
 FRM_HD void log_split_(float x, float* f_out, float* e_out) {
   int e;
   float m = frexpf(x, &e);  // m in [0.5, 1), exact
@@ -144,30 +166,29 @@ FRM_HD float log_special_(float x, float r) {
 FRM_HD float log2_(float x) {
   float f, fe;
   log_split_(x, &f, &fe);
-  float r = fma_(log1p_kernel_(f), kLog2e, fe);
-  return log_special_(x, r);
+  return log_special_(x, fma_(f, log2_poly(f), fe));
+}
+// ln of m 2^e from its split
+FRM_HD float ln_from_split_(float f, float fe) {
+  return fma_(fe, 0.693359375f, fma_(fe, -2.12194440e-4f, f * ln_poly(f)));
 }
 // log_ for positive finite x (normal or subnormal), where log_special_ changes nothing.
 FRM_HD float log_posfinite_(float x) {
   float f, fe;
   log_split_(x, &f, &fe);
-  float l = log1p_kernel_(f);
-  return fma_(fe, 0.693359375f, fma_(fe, -2.12194440e-4f, l));
+  return ln_from_split_(f, fe);
 }
 FRM_HD float log_(float x) { return log_special_(x, log_posfinite_(x)); }
 
 // ---- exp2 / pow -------------------------------------------------------------
 // k = rint(y) after clamping y to [-151, 129]; f = y - k in [-1/2, 1/2] (exact);
-// 2^f = 1 + f*P(f), P degree 5; result = ldexp(2^f, k) (exact scaling, one rounding for
-// subnormal results). NaN in -> NaN out.
+// 2^f = 1 + f P(f); result = ldexp(2^f, k) (exact scaling, one rounding for subnormal
+// results). NaN in -> NaN out.
 FRM_HD float exp2_(float y) {
   float yc = min_(max_(y, -151.0f), 129.0f);
   float k = rintf(yc);
   float f = yc - k;
-  float p = fma_(fma_(fma_(fma_(fma_(1.535336188319500e-4f, f, 1.339887440266574e-3f), f,
-                               9.618437357674640e-3f), f, 5.550332471162809e-2f), f,
-                     2.402264791363012e-1f), f, 6.931472028550421e-1f);
-  float r = ldexpf(fma_(f, p, 1.0f), (int)k);
+  float r = ldexpf(fma_(f, exp2_poly(f), 1.0f), (int)k);
   return (y != y) ? y : r;
 }
 // WGSL pow accuracy is "inherited from exp2(e2 * log2(e1))"; frm defines it as exactly that.

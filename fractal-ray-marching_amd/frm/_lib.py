@@ -23,6 +23,7 @@ FRM_ERR_COMPILE = 8
 
 FRM_NUM_SCENES = 19
 FRM_MAX_FRAMES_IN_FLIGHT = 8
+FRM_MAX_DEVICES = 16
 FRM_MAX_BATCH = 32
 FRM_DEFAULT_MAX_STEPS = 5000
 FRM_MAX_STEPS_LIMIT = 4194303
@@ -58,6 +59,8 @@ class FrmConfig(ctypes.Structure):
         ("max_steps", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
         ("frames_in_flight", ctypes.c_uint32),
+        ("device_count", ctypes.c_uint32),  # ABI 5: a group context over devices[0..count-1]
+        ("devices", ctypes.c_int32 * 16),
     ]
 
 
@@ -123,6 +126,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint64)]),
     ("frm_frame_pixels", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, _P(ctypes.POINTER(ctypes.c_uint8)), _P(ctypes.c_size_t)]),
+    ("frm_group_band_rows", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint32)]),
     ("frm_band_rows_for", ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P(ctypes.c_uint32)]),
     ("frm_render_bands", ctypes.c_int,

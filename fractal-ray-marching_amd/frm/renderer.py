@@ -11,12 +11,24 @@ from . import _lib
 
 
 class Renderer:
-    def __init__(self, device=0, max_steps=0, flags=0, frames_in_flight=1):
+    def __init__(self, device=0, max_steps=0, flags=0, frames_in_flight=1, devices=None):
+        """devices: a list of HIP device ordinals for a GROUP context (frm_config.device_count):
+        every frame is row-tiled over them and gathered on devices[0] (RCCL, or device copies
+        when a device repeats); the rest of the API is the same."""
         lib = _lib.load()
         self._lib = lib
         self.ctx = ctypes.c_void_p()
         cfg = _lib.FrmConfig(device, max_steps, flags, frames_in_flight)
+        if devices is not None:
+            devices = list(devices)
+            if not 1 <= len(devices) <= 16:
+                raise ValueError("a group holds 1..16 devices")
+            cfg.device_count = len(devices)
+            for i, d in enumerate(devices):
+                cfg.devices[i] = d
+            device = devices[0]
         _lib.check(lib.frm_create(ctypes.byref(self.ctx), ctypes.byref(cfg)))
+        self.devices = devices
         self.device = device
         self.frames_in_flight = max(1, frames_in_flight)
         self.width = self.height = 0
@@ -137,8 +149,8 @@ class Renderer:
         self._check(self._lib.frm_render_bands(self.ctx, dev_ptr, nbytes, band_rows, first_band,
                                                band_stride, stream or None, dev_counters or None))
 
-    def render_bands_batch(self, params_list, dev_ptr, dst_bytes, frame_stride, band_rows, first_band, band_stride,
-                           stream=0, dev_counters=0):
+    def render_bands_batch(self, params_list, dev_ptr, *, dst_bytes, frame_stride, band_rows, first_band,
+                           band_stride, stream=0, dev_counters=0):
         """frm_render_bands_batch: len(params_list) frames (same scene; the camera, and for the
         Mandelbulb the time, may differ) in
         one launch, frame k at dev_ptr + k * frame_stride; dst_bytes = the size of the buffer at

@@ -13,8 +13,9 @@
  *     or panics across the ABI. The message of the last failure on a context is
  *     available from frm_last_error(); failures before a context exists are available
  *     from frm_last_error(NULL) (thread-local).
- *   - A context drives one GPU and is not thread-safe (one context per host thread),
- *     mirroring the reference's single winit event-loop thread (src/app.rs).
+ *   - A context drives one GPU, or with frm_config.device_count a group of GPUs row-tiling
+ *     each frame, and is not thread-safe (one context per host thread), mirroring the
+ *     reference's single winit event-loop thread (src/app.rs).
  *   - Rendering is stream-ordered. frm_render() with a NULL stats pointer is
  *     asynchronous; frm_read_frame()/frm_synchronize() wait for it. With
  *     frames_in_flight > 1, consecutive frm_render() calls run on rotating streams and
@@ -34,10 +35,11 @@
 extern "C" {
 #endif
 
-#define FRM_ABI_VERSION 4u  /* 2: frm_config.frames_in_flight (was reserved); 3: frm_render_bands_batch
+#define FRM_ABI_VERSION 5u  /* 2: frm_config.frames_in_flight (was reserved); 3: frm_render_bands_batch
                                takes dst_bytes, frm_set_parameters bounds the fractal loop work;
                                4: asynchronous readback (frm_read_frame_async, frm_present_async,
-                               frm_frame_pixels) */
+                               frm_frame_pixels); 5: frm_config.device_count / devices (one context
+                               row-tiles every frame over several GPUs, RCCL gather) */
 
 /* ---- status codes -------------------------------------------------------- */
 enum {
@@ -132,9 +134,27 @@ typedef struct frm_config {
                          framebuffer and a stream), so frame k+1 runs while frame k's longest
                          pixels finish instead of after them. No reference counterpart: the
                          reference renders one frame per submit (graphics.rs:91-110).        */
+  uint32_t device_count; /* 0: one GPU, `device` (every field above as before). 1..FRM_MAX_DEVICES:
+                         a GROUP context over devices[0..device_count-1] (`device` ignored): every
+                         frm_render row-tiles the frame over those GPUs (device r renders the
+                         interleaved bands r, r+N, ..., as frm_render_bands with first_band r and
+                         band_stride N), gathers the bands on devices[0] with RCCL point-to-point
+                         transfers over xGMI (grouped ncclSend/ncclRecv; device-to-device copies
+                         when a device is listed twice, e.g. to rehearse N ranks on one GPU) and
+                         reassembles the frame there; frm_read_frame, frm_present and their async
+                         forms then see the whole frame, exactly as on one GPU. The per-rank band
+                         entry points (frm_render_bands*, frm_unshuffle_bands, frm_debug_trace,
+                         frm_debug_*_pixel_keys) are FRM_ERR_UNSUPPORTED on a group. No reference
+                         counterpart (the reference is single-device, graphics.rs:25-37).       */
+  int32_t devices[16];  /* HIP device ordinals of a group (FRM_MAX_DEVICES)                        */
 } frm_config;
 
 #define FRM_MAX_FRAMES_IN_FLIGHT 8u
+#define FRM_MAX_DEVICES 16u
+/* Band height a group context uses for a frame of `height` rows over `devices` GPUs: the smallest
+ * height >= 16 that splits the frame into a multiple of `devices` bands (else 16), so the
+ * interleaved bands balance the devices' work. */
+int frm_group_band_rows(uint32_t height, uint32_t devices, uint32_t* out_band_rows);
 /* largest frm_config.max_steps: the persistent kernel packs a pixel's primary step count
    into 22 bits of its 8-byte record (the reference's MAX_ITERATIONS is 5000) */
 #define FRM_MAX_STEPS_LIMIT 4194303u

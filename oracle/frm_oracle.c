@@ -64,60 +64,77 @@ static float wclamp(float x, float lo, float hi) { return wmin(wmax(x, lo), hi);
 static float wmix(float a, float b, float t) { return a * (1.0f - t) + b * t; }
 static float wfract(float x) { return x - floorf(x); }
 
-/* ======================= builtins, OM_FRM (DESIGN.md §frm math) ===================== */
+/* ======================= builtins, OM_FRM (frm semantics v2) ========= */
 static const float PI_F = 3.14159274101257324219f;
 static const float HALF_PI_F = 1.57079637050628662109f;
-static const float HALF_PI_LO_F = -4.37113900018624283e-8f;
+static const float INV_PI_HI = 0x1.45f306p-2f; /* RN(1/pi) */
+static const float INV_PI_LO = 0x1.b93910p-27f; /* RN(1/pi - INV_PI_HI) */
+static const float ROUND_K = 0x1.8p23f;         /* 1.5 * 2^23: x + K rounds x to an integer */
 
-static void frm_sincos(float x, float* so, float* co) {
-  float j = rintf(x * 0.636619746685028076172f);
-  float r = fmaf(-j, HALF_PI_F, x);
-  r = fmaf(-j, HALF_PI_LO_F, r);
-  int q = (int)fminf(fmaxf(j, -4194304.0f), 4194304.0f);
-  float z = r * r;
-  float s = fmaf(r * z, fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), r);
-  float c = fmaf(z * z, fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
-                 fmaf(-0.5f, z, 1.0f));
-  float sv = (q & 1) ? c : s, cv = (q & 1) ? s : c;
-  *so = (q & 2) ? -sv : sv;
-  *co = ((q + 1) & 2) ? -cv : cv;
+static float horner(const float* c, int n, float x) { /* c[0] + x (c[1] + x (... c[n-1])) */
+  float p = c[n - 1];
+  for (int i = n - 2; i >= 0; --i) p = fmaf(p, x, c[i]);
+  return p;
 }
 
+/* sin/cos: half-turn reduction r = x/pi - j, j the nearest integer (|r| <= 1/2);
+ * sin(x) = (-1)^j r S(r^2), cos(x) = (-1)^j C(r^2), minimax fits of sin(pi r)/r and cos(pi r)
+ * (tools/v2fit.py). For |x| <= 2^20, j = rint of the exact product x * INV_PI_HI, taken from
+ * t = fma(x, INV_PI_HI, K) (t's unit in the last place is 1); larger or non-finite x take
+ * j = rint(RN(x * INV_PI_HI)) (defined, not accurate: WGSL bounds sin/cos on [-pi, pi] only). */
+static const float SIN_C[5] = {0x1.921fb6p+1f, -0x1.4abbc2p+2f, 0x1.4668b0p+1f, -0x1.324cccp-1f, 0x1.3daffap-4f};
+static const float COS_C[5] = {1.0f, -0x1.3bd3b0p+2f, 0x1.03bdaap+2f, -0x1.55041ap+0f, 0x1.c2b9aap-3f};
+static void frm_sincos(float x, float* so, float* co) {
+  float j;
+  int odd;
+  if (fabsf(x) <= 0x1p20f) {
+    float t = fmaf(x, INV_PI_HI, ROUND_K);
+    uint32_t tb;
+    memcpy(&tb, &t, 4);
+    j = t - ROUND_K;
+    odd = (int)(tb & 1u);
+  } else {
+    j = rintf(x * INV_PI_HI);
+    odd = fabsf(j) < 0x1p24f ? (int)((int64_t)j & 1) : 0; /* NaN: 0 */
+  }
+  float r = fmaf(x, INV_PI_HI, -j);
+  r = fmaf(x, INV_PI_LO, r);
+  float u = r * r;
+  float s = r * horner(SIN_C, 5, u);
+  float c = horner(COS_C, 5, u);
+  *so = odd ? -s : s;
+  *co = odd ? -c : c;
+}
+
+/* acos(t) = sqrt(1 - |t|) P(|t|) for t >= 0 and pi - that for t < 0; P a relative minimax fit
+ * with P(0) = RN(pi/2). */
+static const float ACOS_C[7] = {0x1.921fb6p+0f, -0x1.b77b98p-3f, 0x1.6bbdc6p-4f, -0x1.912814p-5f,
+                                0x1.bd48d6p-6f, -0x1.748422p-7f, 0x1.35deb4p-9f};
 static float frm_acos(float t) {
   float a = fabsf(t);
-  int big = a > 0.5f;
-  float zb = 0.5f * (1.0f - a);
-  float z = big ? zb : a * a;
-  float w = big ? sqrtf(zb) : a;
-  float p = fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z, 7.4953002686e-2f), z,
-                 1.6666752422e-1f);
-  float s = fmaf(w * z, p, w);
-  if (big) return t > 0.0f ? 2.0f * s : PI_F - 2.0f * s;
-  return HALF_PI_F - copysignf(s, t);
+  float r = sqrtf(1.0f - a) * horner(ACOS_C, 7, a);
+  return t < 0.0f ? PI_F - r : r;
 }
 
+/* atan2: a = min(|x|,|y|) * RN(1 / max(|x|,|y|)) in [0, 1] (0 when both are 0);
+ * atan(a) = a + a s Q(s), s = a^2, Q a relative minimax fit; octant and quadrant fix-ups;
+ * atan2(+-0, +-0) = +-0. */
+static const float ATAN_C[7] = {-0x1.5552dep-2f, 0x1.991268p-3f, -0x1.1f90fcp-3f, 0x1.984ef0p-4f,
+                                -0x1.ed2edep-5f, 0x1.953dcap-6f, -0x1.3c0c38p-8f};
 static float frm_atan2(float y, float x) {
   float ax = fabsf(x), ay = fabsf(y);
   float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-  float a = mn / mx;
+  float a = mn * (1.0f / mx);
   if (mx == 0.0f) a = 0.0f;
   float s = a * a;
-  float q = 0.002974590389872539f;
-  q = fmaf(q, s, -0.016581183968493302f);
-  q = fmaf(q, s, 0.04355353931255974f);
-  q = fmaf(q, s, -0.07580578130128461f);
-  q = fmaf(q, s, 0.10678940285181907f);
-  q = fmaf(q, s, -0.14214209135918496f);
-  q = fmaf(q, s, 0.1999413720560495f);
-  q = fmaf(q, s, -0.3333316696611865f);
-  float r = fmaf(a * s, q, a);
+  float r = fmaf(a * s, horner(ATAN_C, 7, s), a);
   if (ay > ax) r = HALF_PI_F - r;
   if (x < 0.0f) r = PI_F - r;
   return copysignf(r, y);
 }
 
-/* x = m 2^e, m in [sqrt(1/2), sqrt(2)); returns ln(m) and e */
-static float frm_ln_mantissa(float x, float* e_out) {
+/* x = m 2^e, m in [sqrt(1/2), sqrt(2)); returns f = m - 1 (exact) and e */
+static float frm_split(float x, float* e_out) {
   int e;
   float m = frexpf(x, &e);
   if (m < 0.707106769084930419922f) {
@@ -125,18 +142,7 @@ static float frm_ln_mantissa(float x, float* e_out) {
     e = e - 1;
   }
   *e_out = (float)e;
-  float f = m - 1.0f;
-  float z = f * f;
-  float p = 7.0376836292e-2f;
-  p = fmaf(p, f, -1.1514610310e-1f);
-  p = fmaf(p, f, 1.1676998740e-1f);
-  p = fmaf(p, f, -1.2420140846e-1f);
-  p = fmaf(p, f, 1.4249322787e-1f);
-  p = fmaf(p, f, -1.6668057665e-1f);
-  p = fmaf(p, f, 2.0000714765e-1f);
-  p = fmaf(p, f, -2.4999993993e-1f);
-  p = fmaf(p, f, 3.3333331174e-1f);
-  return f + fmaf(-0.5f, z, (f * z) * p);
+  return m - 1.0f;
 }
 static float frm_log_special(float x, float r) {
   if (x != x || x < 0.0f) return NAN;
@@ -144,28 +150,32 @@ static float frm_log_special(float x, float r) {
   if (x == INFINITY) return INFINITY;
   return r;
 }
+/* log2(x) = e + f Q(f), Q a relative minimax fit of log2(1 + f) / f */
+static const float LOG2_C[8] = {0x1.715476p+0f, -0x1.715528p-1f, 0x1.ec7724p-2f, -0x1.70e2aap-2f,
+                                0x1.25fd38p-2f, -0x1.fdb316p-3f, 0x1.df5156p-3f, -0x1.2a9f30p-3f};
 static float frm_log2(float x) {
   float e;
-  float l = frm_ln_mantissa(x, &e);
-  return frm_log_special(x, fmaf(l, 1.44269502162933349609f, e));
+  float f = frm_split(x, &e);
+  return frm_log_special(x, fmaf(f, horner(LOG2_C, 8, f), e));
 }
+/* log(x) = e ln2 + f L(f) (ln 2 in two parts), L a relative minimax fit of ln(1 + f) / f */
+static const float LN_C[8] = {0x1.fffffep-1f, -0x1.00007ap-1f, 0x1.5559dcp-2f, -0x1.ff623ep-3f,
+                              0x1.978e32p-3f, -0x1.614bfcp-3f, 0x1.4c3cdcp-3f, -0x1.9dfa4ep-4f};
 static float frm_log(float x) {
   float e;
-  float l = frm_ln_mantissa(x, &e);
+  float f = frm_split(x, &e);
+  float l = f * horner(LN_C, 8, f);
   return frm_log_special(x, fmaf(e, 0.693359375f, fmaf(e, -2.12194440e-4f, l)));
 }
+/* exp2: k = rint(y) after clamping y to [-151, 129], f = y - k in [-1/2, 1/2] (exact);
+ * 2^f = 1 + f P(f) (relative minimax fit); ldexp (one rounding for subnormal results). */
+static const float EXP2_C[5] = {0x1.62e42ap-1f, 0x1.ebf9bcp-3f, 0x1.c6b752p-5f, 0x1.3cea80p-7f, 0x1.5bb9f4p-10f};
 static float frm_exp2(float y) {
   if (y != y) return y;
   float yc = fminf(fmaxf(y, -151.0f), 129.0f);
   float k = rintf(yc);
   float f = yc - k;
-  float p = 1.535336188319500e-4f;
-  p = fmaf(p, f, 1.339887440266574e-3f);
-  p = fmaf(p, f, 9.618437357674640e-3f);
-  p = fmaf(p, f, 5.550332471162809e-2f);
-  p = fmaf(p, f, 2.402264791363012e-1f);
-  p = fmaf(p, f, 6.931472028550421e-1f);
-  return ldexpf(fmaf(f, p, 1.0f), (int)k);
+  return ldexpf(fmaf(f, horner(EXP2_C, 5, f), 1.0f), (int)k);
 }
 
 /* ======================= builtin dispatch ======================================== */

@@ -31,7 +31,7 @@ def test_every_declared_symbol_is_exported(frm_lib):
 
 
 def test_abi_version(frm_lib):
-    assert frm_lib.frm_abi_version() == 4
+    assert frm_lib.frm_abi_version() == 5
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -91,3 +91,42 @@ def test_band_rows_for_matches_tiling(frm_lib, height, band_rows, ranks):
         out = ctypes.c_uint32()
         assert frm_lib.frm_band_rows_for(height, band_rows, rank, ranks, ctypes.byref(out)) == 0
         assert out.value == tiling.rank_rows(height, band_rows, rank, ranks)
+
+
+@pytest.mark.parametrize("height,devices", [(2160, 8), (2160, 4), (2160, 2), (4320, 8), (16384, 8), (1080, 3),
+                                            (7, 2), (100, 16), (2160, 1), (17, 5)])
+def test_group_band_rows_matches_tiling(frm_lib, height, devices):
+    """A group context's row split (frm_config.device_count) uses the band height of frm/tiling.py,
+    the one the multi-process row split uses, and its rank shares cover the frame exactly."""
+    from frm import tiling
+    out = ctypes.c_uint32()
+    assert frm_lib.frm_group_band_rows(height, devices, ctypes.byref(out)) == _lib.FRM_OK
+    assert out.value == tiling.choose_band_rows(height, devices)
+    rows = []
+    for r in range(devices):
+        got = ctypes.c_uint32()
+        assert frm_lib.frm_band_rows_for(height, out.value, r, devices, ctypes.byref(got)) == 0
+        rows.append(got.value)
+    nb = -(-height // out.value)
+    assert sum(rows) == nb * out.value  # every band once (the last one padded to band_rows)
+    assert rows[0] == max(rows)  # rank 0's share sizes the gather buffer's rank stride
+
+
+def test_group_config_errors(frm_lib):
+    L = frm_lib
+    out = ctypes.c_uint32()
+    for h, n in ((0, 2), (2160, 0), (2160, 17)):
+        assert L.frm_group_band_rows(h, n, ctypes.byref(out)) == _lib.FRM_ERR_INVALID_ARGUMENT
+    assert L.frm_group_band_rows(2160, 2, None) == _lib.FRM_ERR_INVALID_ARGUMENT
+    ctx = ctypes.c_void_p()
+    bad = _lib.FrmConfig(0, 0, 0, 1)
+    bad.device_count = _lib.FRM_MAX_DEVICES + 1  # above the device list
+    assert L.frm_create(ctypes.byref(ctx), ctypes.byref(bad)) == _lib.FRM_ERR_INVALID_ARGUMENT
+    assert b"device_count" in L.frm_last_error(None)
+    assert not ctx.value
+    if frm.device_count() == 0:  # no GPU here: a valid group config reports the missing device
+        ok = _lib.FrmConfig(0, 0, 0, 2)
+        ok.device_count = 2
+        assert L.frm_create(ctypes.byref(ctx), ctypes.byref(ok)) == _lib.FRM_ERR_NO_DEVICE
+    with pytest.raises(ValueError):
+        frm.Renderer(devices=[])

@@ -34,7 +34,7 @@ def test_batch_whole_frames_bit_exact(frm_lib, oracle, scene, iters, steps, infl
         for rep in range(3):  # the second and third batches fetch in the scheduled order
             counters.zero_()
             out.zero_()
-            r.render_bands_batch(ps, out.data_ptr(), out.numel(), fb, h, 0, 1, 0, counters.data_ptr())
+            r.render_bands_batch(ps, out.data_ptr(), dst_bytes=out.numel(), frame_stride=fb, band_rows=h, first_band=0, band_stride=1, stream=0, dev_counters=counters.data_ptr())
             torch.cuda.synchronize()
             img = out.cpu().numpy().reshape(len(ps), h, w, 4)
             for k, ref in enumerate(refs):
@@ -59,7 +59,7 @@ def test_batch_band_split_bit_exact(frm_lib, oracle):
         for rep in range(2):
             for rk, rd in enumerate(rds):
                 rd.resize(w, h)
-                rd.render_bands_batch(ps, gathered.data_ptr() + rk * B * nb, B * nb, nb, br, rk, ranks)
+                rd.render_bands_batch(ps, gathered.data_ptr() + rk * B * nb, dst_bytes=B * nb, frame_stride=nb, band_rows=br, first_band=rk, band_stride=ranks)
             torch.cuda.synchronize()
             for b, p in enumerate(ps):
                 frame = torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)
@@ -89,19 +89,19 @@ def test_batch_rejects_frames_that_differ_beyond_the_camera(frm_lib):
         r.resize(w, h)
         for first, other in ((a, c), (m0, m1), (a, d)):
             with pytest.raises(frm.FrmError) as e:
-                r.render_bands_batch([first, other], buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
+                r.render_bands_batch([first, other], buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=w * h * 4, band_rows=h, first_band=0, band_stride=1)
             assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
         with pytest.raises(frm.FrmError):
-            r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
+            r.render_bands_batch([a] * (frm.FRM_MAX_BATCH + 1), buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=w * h * 4, band_rows=h, first_band=0, band_stride=1)
         # the destination must hold every frame: (count - 1) strides + one frame
         for n, stride in ((2, w * h * 4 + 4), (3, w * h * 4)):
             with pytest.raises(frm.FrmError) as e:
-                r.render_bands_batch([a] * n, buf.data_ptr(), buf.numel(), stride, h, 0, 1)
+                r.render_bands_batch([a] * n, buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=stride, band_rows=h, first_band=0, band_stride=1)
             assert e.value.code == _lib.FRM_ERR_BUFFER_TOO_SMALL
         with pytest.raises(frm.FrmError) as e:  # strides of 16 GiB and more do not fit the kernel's word stride
-            r.render_bands_batch([a] * 2, buf.data_ptr(), 1 << 35, 1 << 34, h, 0, 1)
+            r.render_bands_batch([a] * 2, buf.data_ptr(), dst_bytes=1 << 35, frame_stride=1 << 34, band_rows=h, first_band=0, band_stride=1)
         assert e.value.code == _lib.FRM_ERR_INVALID_ARGUMENT
-        r.render_bands_batch([a] * 2, buf.data_ptr(), buf.numel(), w * h * 4, h, 0, 1)
+        r.render_bands_batch([a] * 2, buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=w * h * 4, band_rows=h, first_band=0, band_stride=1)
 
 
 def test_batch_of_max_frames_two_slots(frm_lib, oracle):
@@ -123,7 +123,7 @@ def test_batch_of_max_frames_two_slots(frm_lib, oracle):
         r.resize(w, h)
         for rep in range(3):
             for o in outs:
-                r.render_bands_batch(ps, o.data_ptr(), o.numel(), fb, h, 0, 1, 0, counters.data_ptr())
+                r.render_bands_batch(ps, o.data_ptr(), dst_bytes=o.numel(), frame_stride=fb, band_rows=h, first_band=0, band_stride=1, stream=0, dev_counters=counters.data_ptr())
             torch.cuda.synchronize()
             for j, o in enumerate(outs):
                 img = o.cpu().numpy().reshape(B, h, w, 4)
@@ -143,7 +143,7 @@ def test_batch_rank_without_bands(frm_lib):
     with frm.Renderer(device=0, max_steps=64) as r:
         r.resize(w, h)
         for stride, nbytes in ((0, 0), (4, buf.numel())):
-            r.render_bands_batch([a] * 3, buf.data_ptr(), nbytes, stride, br, 1, ranks, 0, counters.data_ptr())
+            r.render_bands_batch([a] * 3, buf.data_ptr(), dst_bytes=nbytes, frame_stride=stride, band_rows=br, first_band=1, band_stride=ranks, stream=0, dev_counters=counters.data_ptr())
         torch.cuda.synchronize()
         assert int(counters.sum()) == 0 and int(buf.sum()) == 0
 
@@ -175,7 +175,7 @@ def test_batch_animated_mandelbulb_bit_exact(frm_lib, oracle, kernel):
             ps = frames[launch * B:(launch + 1) * B]
             buf = bufs[launch % 2]
             counters.zero_()
-            r.render_bands_batch(ps, buf.data_ptr(), buf.numel(), nb, height, 0, 1, 0, counters.data_ptr())
+            r.render_bands_batch(ps, buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=nb, band_rows=height, first_band=0, band_stride=1, stream=0, dev_counters=counters.data_ptr())
             r.synchronize()
             got = buf.cpu().numpy()
             for b in range(B):

@@ -117,9 +117,9 @@ def _fast_inputs(name, rng):
             a[a == 0] = 0.0
         return "div", a, b
     if name in ("sin_small", "cos_small"):
-        lim = 2.0 ** 22 * np.pi / 2 * 0.999
+        lim = 2.0 ** 20  # sincos_small is sincos_'s |x| <= 2^20 branch (frm_math.h)
         a = np.concatenate([rng.uniform(-30, 30, n), rng.uniform(-lim, lim, n // 4),
-                            [0.0, -0.0, np.pi, -np.pi, 9 * np.pi, lim, -lim]])
+                            [0.0, -0.0, np.pi, -np.pi, 9 * np.pi, lim, -lim, np.pi / 2, 0.5, -1.5]])
         return name.split("_")[0], a, None
     if name == "acos_dev":
         return "acos", np.concatenate([rng.uniform(-1, 1, n), [1, -1, 0.5, -0.5, 0.0, -0.0, 1.0000001, np.nan]]), None

@@ -171,7 +171,7 @@ def test_fly_through_batched_matches_golden(frm_lib):
         r.resize(w.width, w.height)
         for rep in range(2):
             counters.zero_()
-            r.render_bands_batch(ps, buf.data_ptr(), buf.numel(), nb, w.height, 0, 1, 0, counters.data_ptr())
+            r.render_bands_batch(ps, buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=nb, band_rows=w.height, first_band=0, band_stride=1, stream=0, dev_counters=counters.data_ptr())
             r.synchronize()
             host = buf.cpu().numpy()
             for b, key in enumerate(keys):
@@ -211,8 +211,8 @@ def _split_frames(name, ranks, params_list, batch, inflight):
             for r, rd in enumerate(rds):
                 buf = gathered[r * n:(r + 1) * n]
                 if batch > 1:
-                    rd.render_bands_batch(ps, buf.data_ptr(), buf.numel(), nbytes, band_rows, r, ranks, 0,
-                                          counters.data_ptr())
+                    rd.render_bands_batch(ps, buf.data_ptr(), dst_bytes=buf.numel(), frame_stride=nbytes, band_rows=band_rows, first_band=r, band_stride=ranks, stream=0,
+                                          dev_counters=counters.data_ptr())
                 else:
                     rd.update_parameters_buffer(ps[0])
                     rd.render_bands(buf.data_ptr(), n, band_rows, r, ranks, 0, counters.data_ptr())

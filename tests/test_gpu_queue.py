@@ -47,7 +47,7 @@ def test_multi_frame_launch_claims_every_chunk_once(frm_lib, oracle, chunks, bat
         r.resize(w, h)
         for rep in range(2):
             counters.zero_()
-            r.render_bands_batch(ps, out.data_ptr(), out.numel(), fb, h, 0, 1, 0, counters.data_ptr())
+            r.render_bands_batch(ps, out.data_ptr(), dst_bytes=out.numel(), frame_stride=fb, band_rows=h, first_band=0, band_stride=1, stream=0, dev_counters=counters.data_ptr())
             torch.cuda.synchronize()
             img = out.cpu().numpy().reshape(batch, h, w, 4)
             for k, ref in enumerate(refs):

@@ -73,8 +73,8 @@ def run(workload, ranks, rank, inflight, frames, warmup, mode="slots", events=Fa
             if events:
                 torch.cuda.Event(enable_timing=True).record(ss[i])
             if batch > 1:
-                rs[i].render_bands_batch([p] * batch, bufs[i].data_ptr(), bufs[i].numel(), fbytes, br, rank, ranks,
-                                         ss[i].cuda_stream, counters.data_ptr())
+                rs[i].render_bands_batch([p] * batch, bufs[i].data_ptr(), dst_bytes=bufs[i].numel(), frame_stride=fbytes, band_rows=br, first_band=rank, band_stride=ranks,
+                                         stream=ss[i].cuda_stream, dev_counters=counters.data_ptr())
             else:
                 rs[i].render_bands(bufs[i].data_ptr(), bufs[i].numel(), br, rank, ranks, ss[i].cuda_stream,
                                    counters.data_ptr())
