@@ -91,6 +91,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
                     "copy of csrc/ (frm_reload, hiprtc)")
+    ap.add_argument("--mode", default="ranks", choices=["ranks", "group"],
+                    help="ranks: one process per GPU (torch.distributed.run, the driver's runs); group: ONE "
+                    "process drives all --gpus devices through a group context (frm_config.device_count: "
+                    "every frm_render row-tiles the frame over the devices, gathers the bands on device 0 "
+                    "with RCCL and reassembles it), the path a C or Rust host binding include/frm.h takes "
+                    "(INTEGRATION.md section 3); FRM_BENCH_GROUP_DEVICES=0,0,0 lists the devices explicitly "
+                    "(a repeated device rehearses ranks on one GPU with device copies)")
     return ap.parse_args()
 
 
@@ -340,8 +347,91 @@ def counters_check(counters, workload, pose, frames, golden_path=GOLDEN):
             **({"counters_mismatch": bad} if bad else {})}
 
 
+def group_bench(args):
+    """--mode group: one process, one group context over --gpus devices (include/frm.h ABI 5). The
+    timed region is --steps frm_render calls (frames_in_flight slots rotate; each frame's bands are
+    rendered on every device, gathered on device 0 and reassembled there) bracketed by
+    frm_synchronize; march steps come from an untimed pass with stats over the same frames."""
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    import torch  # noqa: F401  (one HIP runtime: libfrm binds to torch's, DESIGN.md section 9)
+    import frm
+
+    w = frm.WORKLOADS[args.workload]
+    env = os.environ.get("FRM_BENCH_GROUP_DEVICES")
+    devices = [int(v) for v in env.split(",")] if env else list(range(args.gpus))
+    if len(devices) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but FRM_BENCH_GROUP_DEVICES lists {len(devices)} devices")
+    inflight = max(1, min(args.inflight or 3, frm.FRM_MAX_FRAMES_IN_FLIGHT))
+    flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
+        {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel])
+    seq = frm.frame_sequence(w, pose=args.pose)
+    frames = [next(seq) for _ in range(args.steps)] if w.moving else [next(seq)] * args.steps
+    with frm.Renderer(max_steps=w.max_steps, flags=flags, frames_in_flight=inflight, devices=devices) as r:
+        r.resize(w.width, w.height)
+        for _ in range(max(1, args.warmup)):
+            r.update_parameters_buffer(frames[0])
+            r.render(stats=False)
+        r.synchronize()
+        t0 = time.perf_counter()
+        for p in frames:
+            r.update_parameters_buffer(p)
+            r.render(stats=False)
+        r.synchronize()
+        elapsed = time.perf_counter() - t0
+        steps_total = 0
+        counters = [0] * len(COUNTER_NAMES)
+        for k, p in enumerate(frames):
+            r.update_parameters_buffer(p)
+            st = r.render(stats=True)
+            steps_total += st["march_steps"]
+            counters = [a + st[n] for a, n in zip(counters, COUNTER_NAMES)]
+            if k == 0:
+                import numpy as np
+                sha = hashlib.sha256(np.ascontiguousarray(r.read_frame()).tobytes()).hexdigest()
+                if w.moving:
+                    break
+        if w.moving:  # the stats pass rendered frame 0 only
+            steps_total = None
+    key = golden_key(args.workload, args.pose)
+    gold = json.load(open(GOLDEN)).get(key) if os.path.exists(GOLDEN) else None
+    out = {
+        "metric": METRIC,
+        "value": None if steps_total is None else steps_total / elapsed / 1e9,
+        "unit": "Gray-march-steps/s",
+        "n_gpus": len(devices),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: deterministic Parameters (" + motion(w) + "), no input data",
+        "config": {"workload": w.name, "width": w.width, "height": w.height, "scene_index": w.scene,
+                   "num_iterations": w.iters, "max_steps": w.max_steps, "pose": args.pose,
+                   "frames_in_flight": inflight, "frames_per_launch": 1, "devices": devices,
+                   "parallelism": f"group context over {len(devices)} devices: row bands + "
+                                  + ("RCCL point-to-point gather" if len(set(devices)) == len(devices) > 1 else
+                                     "device-copy gather" if len(devices) > 1 else "no gather (one device)")
+                                  + " to device 0, reassembled there (one process)"},
+        "launcher": "single process (--mode group, frm_config.device_count)",
+        "frames_per_sec": args.steps / elapsed,
+        "frame_sha256": sha,
+        "frame_sha_ok": None if gold is None else sha == gold["sha256"],
+        "frame_golden": None if gold is None else f"tests/golden/fullsize.json[{key}]",
+    }
+    if not w.moving:
+        cc = counters_check(counters, args.workload, args.pose, args.steps)
+        if cc is not None:
+            out.update(cc)
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
+    if args.mode == "group":
+        return group_bench(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args)
     # before torch initialises HIP

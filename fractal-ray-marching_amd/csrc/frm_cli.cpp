@@ -12,13 +12,12 @@
 // With --batch B (one context) the fly-through's frames are rendered B per launch
 // (frm_render_bands_batch: one work queue for B frames whose camera and, for the Mandelbulb,
 // time differ), so a launch's tail is paid once per B frames; the frames' bytes are the same.
-// With --gpus N every frame is row-tiled across devices 0..N-1 from this one process
-// (ncclCommInitAll over the node's devices): device r renders the
-// interleaved bands r, r+N, ... (frm_render_bands), RCCL point-to-point sends gather the
-// band buffers on device 0 over xGMI, and device 0 reassembles the frame
-// (frm_unshuffle_bands). The C host a Rust or C caller would write, without Python.
+// With --gpus N every frame is row-tiled across devices 0..N-1 from this one process: the CLI
+// creates a group context (frm_config.device_count = N, include/frm.h), in which device r renders
+// the interleaved bands r, r+N, ..., RCCL point-to-point transfers gather the bands on device 0
+// over xGMI and device 0 reassembles the frame. Everything else is the one-GPU
+// loop: frm_render + frm_read_frame, the config alone selects the GPUs.
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -34,12 +33,6 @@ static void hip_check(hipError_t e, const char* what) {
     exit(1);
   }
 }
-static void nccl_check(ncclResult_t e, const char* what) {
-  if (e != ncclSuccess) {
-    fprintf(stderr, "frm_render: %s failed: %s\n", what, ncclGetErrorString(e));
-    exit(1);
-  }
-}
 
 static int check(int rc, frm_ctx* ctx, const char* what) {
   if (rc != FRM_OK) {
@@ -48,100 +41,6 @@ static int check(int rc, frm_ctx* ctx, const char* what) {
   }
   return rc;
 }
-
-// Smallest band height >= 16 that splits the frame into a multiple of `ranks` bands (else
-// 16): interleaved bands balance the ranks' work (frm/tiling.py choose_band_rows).
-static uint32_t choose_band_rows(uint32_t height, uint32_t ranks) {
-  for (uint32_t br = 16; br <= height; ++br)
-    if (height % br == 0 && (height / br) % ranks == 0) return br;
-  return 16;
-}
-
-// One frame row-tiled across devices 0..n-1 of this process, gathered on device 0.
-struct RowTiled {
-  uint32_t n = 0, width = 0, height = 0, band_rows = 0;
-  size_t stride = 0;  // bytes of every device's band buffer (the largest share, padded)
-  std::vector<frm_ctx*> ctx;
-  std::vector<hipStream_t> stream;
-  std::vector<uint8_t*> buf;
-  std::vector<uint64_t*> counters;
-  std::vector<ncclComm_t> comm;
-  uint8_t* gathered = nullptr;  // device 0: n * stride
-  uint8_t* frame = nullptr;     // device 0: width * height * 4
-
-  void init(uint32_t gpus, uint32_t w, uint32_t h, uint32_t max_steps, uint32_t flags) {
-    n = gpus, width = w, height = h;
-    band_rows = choose_band_rows(h, n);
-    uint32_t rows0 = 0;
-    check(frm_band_rows_for(h, band_rows, 0, n, &rows0), nullptr, "frm_band_rows_for");
-    stride = (size_t)rows0 * w * 4;
-    ctx.resize(n), stream.resize(n), buf.resize(n), counters.resize(n), comm.resize(n);
-    std::vector<int> devs(n);
-    for (uint32_t r = 0; r < n; ++r) {
-      devs[r] = (int)r;
-      frm_config cfg = {(int32_t)r, max_steps, flags, 1};
-      check(frm_create(&ctx[r], &cfg), nullptr, "frm_create");
-      check(frm_resize(ctx[r], w, h), ctx[r], "frm_resize");
-      hip_check(hipSetDevice((int)r), "hipSetDevice");
-      hip_check(hipStreamCreateWithFlags(&stream[r], hipStreamNonBlocking), "hipStreamCreate");
-      hip_check(hipMalloc(&buf[r], stride), "hipMalloc(bands)");
-      hip_check(hipMalloc(&counters[r], FRM_NUM_COUNTERS * sizeof(uint64_t)), "hipMalloc(counters)");
-    }
-    hip_check(hipSetDevice(0), "hipSetDevice");
-    hip_check(hipMalloc(&gathered, n * stride), "hipMalloc(gathered)");
-    hip_check(hipMalloc(&frame, (size_t)w * h * 4), "hipMalloc(frame)");
-    nccl_check(ncclCommInitAll(comm.data(), (int)n, devs.data()), "ncclCommInitAll");
-  }
-
-  // Renders, gathers and reassembles one frame; returns the summed work counters.
-  void render(const frm_parameters& p, uint8_t* host_rgba, uint64_t* sums) {
-    for (uint32_t r = 0; r < n; ++r) {
-      check(frm_set_parameters(ctx[r], &p), ctx[r], "frm_set_parameters");
-      hip_check(hipSetDevice((int)r), "hipSetDevice");
-      hip_check(hipMemsetAsync(counters[r], 0, FRM_NUM_COUNTERS * sizeof(uint64_t), stream[r]),
-                "hipMemsetAsync");
-      check(frm_render_bands(ctx[r], buf[r], stride, band_rows, r, n, stream[r], counters[r]), ctx[r],
-            "frm_render_bands");
-    }
-    // gather on device 0: rank-major band buffers, one point-to-point transfer per peer
-    nccl_check(ncclGroupStart(), "ncclGroupStart");
-    for (uint32_t r = 0; r < n; ++r) {
-      hip_check(hipSetDevice((int)r), "hipSetDevice");
-      nccl_check(ncclSend(buf[r], stride, ncclUint8, 0, comm[r], stream[r]), "ncclSend");
-      if (r == 0)
-        for (uint32_t s = 0; s < n; ++s)
-          nccl_check(ncclRecv(gathered + s * stride, stride, ncclUint8, (int)s, comm[0], stream[0]), "ncclRecv");
-    }
-    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-    hip_check(hipSetDevice(0), "hipSetDevice");
-    check(frm_unshuffle_bands(ctx[0], gathered, stride, frame, (size_t)width * height * 4, band_rows, n, stream[0]),
-          ctx[0], "frm_unshuffle_bands");
-    hip_check(hipMemcpyAsync(host_rgba, frame, (size_t)width * height * 4, hipMemcpyDeviceToHost, stream[0]),
-              "hipMemcpyAsync");
-    for (uint32_t k = 0; k < FRM_NUM_COUNTERS; ++k) sums[k] = 0;
-    for (uint32_t r = 0; r < n; ++r) {
-      uint64_t c[FRM_NUM_COUNTERS];
-      hip_check(hipSetDevice((int)r), "hipSetDevice");
-      hip_check(hipMemcpyAsync(c, counters[r], sizeof(c), hipMemcpyDeviceToHost, stream[r]), "hipMemcpyAsync");
-      hip_check(hipStreamSynchronize(stream[r]), "hipStreamSynchronize");
-      for (uint32_t k = 0; k < FRM_NUM_COUNTERS; ++k) sums[k] += c[k];
-    }
-  }
-
-  void destroy() {  // best effort, statuses ignored
-    for (uint32_t r = 0; r < n; ++r) {
-      (void)hipSetDevice((int)r);
-      (void)ncclCommDestroy(comm[r]);
-      (void)hipFree(buf[r]);
-      (void)hipFree(counters[r]);
-      (void)hipStreamDestroy(stream[r]);
-      frm_destroy(ctx[r]);
-    }
-    (void)hipSetDevice(0);
-    (void)hipFree(gathered);
-    (void)hipFree(frame);
-  }
-};
 
 static int write_ppm(const char* out, uint32_t fr, const uint8_t* rgba, uint32_t width, uint32_t height,
                      char* name, size_t name_len) {
@@ -220,7 +119,7 @@ int main(int argc, char** argv) {
   uint32_t frames = 1, keys = 0;
   float dt = 1.0f / 60.0f, orbit = 0.0f, time_factor = 1.0f;
   int lock_yaw = FRM_LOCK_YAW_NONE, lock_pitch = 0;
-  uint32_t gpus = 0;  // 0: one context, frm_render; >= 1: row-tiled across devices + RCCL
+  uint32_t gpus = 0;  // 0: one GPU (--device); >= 1: a group context over devices 0..gpus-1
   uint32_t batch = 1;  // frames per launch (one context)
   for (int i = 1; i < argc; ++i) {
     const char* a = argv[i];
@@ -253,19 +152,18 @@ int main(int argc, char** argv) {
     else { fprintf(stderr, "unknown argument %s\n", a); return 2; }
   }
   frm_ctx* ctx = nullptr;
-  RowTiled tiled;
+  frm_config cfg = {device, max_steps, flags, 0, 0, {0}};
   if (gpus > 0) {
     int count = 0;
     hip_check(hipGetDeviceCount(&count), "hipGetDeviceCount");
-    if ((int)gpus > count) {
-      fprintf(stderr, "frm_render: --gpus %u but %d devices\n", gpus, count);
+    if ((int)gpus > count || gpus > FRM_MAX_DEVICES) {
+      fprintf(stderr, "frm_render: --gpus %u but %d devices (at most %u)\n", gpus, count, FRM_MAX_DEVICES);
       return 2;
     }
-    tiled.init(gpus, width, height, max_steps, flags);
-  } else {
-    frm_config cfg = {device, max_steps, flags, 0};
-    check(frm_create(&ctx, &cfg), nullptr, "frm_create");
+    cfg.device_count = gpus;  // a group context: devices 0..gpus-1
+    for (uint32_t r = 0; r < gpus; ++r) cfg.devices[r] = (int32_t)r;
   }
+  check(frm_create(&ctx, &cfg), nullptr, "frm_create");
   frm_parameters p;
   frm_parameters_default(&p);
   frm_parameters_update_aspect(&p, width, height);
@@ -284,13 +182,17 @@ int main(int argc, char** argv) {
   frm_timing_init(&timing);
   timing.time_factor = time_factor;
   frm_parameters_update_camera_from(&p, &cam);
-  if (ctx) check(frm_resize(ctx, width, height), ctx, "frm_resize");
+  check(frm_resize(ctx, width, height), ctx, "frm_resize");
   std::vector<uint8_t> rgba((size_t)width * height * 4);
   if (batch < 1 || batch > FRM_MAX_BATCH) {
     fprintf(stderr, "frm_render: --batch %u outside [1, %u]\n", batch, FRM_MAX_BATCH);
     return 2;
   }
-  if (batch > 1 && ctx) return render_batched(ctx, p, cam, timing, keys, dt, frames, batch, width, height, out);
+  if (batch > 1 && gpus > 0) {
+    fprintf(stderr, "frm_render: --batch renders on one GPU (frm_render_bands_batch is a per-device entry point)\n");
+    return 2;
+  }
+  if (batch > 1) return render_batched(ctx, p, cam, timing, keys, dt, frames, batch, width, height, out);
   for (uint32_t fr = 0; fr < frames; ++fr) {
     if (fr > 0) {  // initialized_app.rs:43-48, with a fixed frame time
       const float delta = frm_timing_update(&timing, &p, dt);
@@ -299,30 +201,9 @@ int main(int argc, char** argv) {
     }
     frm_stats st;
     memset(&st, 0, sizeof(st));
-    if (ctx) {
-      check(frm_set_parameters(ctx, &p), ctx, "frm_set_parameters");
-      check(frm_render(ctx, &st), ctx, "frm_render");
-      check(frm_read_frame(ctx, rgba.data(), rgba.size()), ctx, "frm_read_frame");
-    } else {
-      uint64_t c[FRM_NUM_COUNTERS];
-      hipEvent_t t0, t1;
-      hip_check(hipSetDevice(0), "hipSetDevice");
-      hip_check(hipEventCreate(&t0), "hipEventCreate");
-      hip_check(hipEventCreate(&t1), "hipEventCreate");
-      hip_check(hipEventRecord(t0, tiled.stream[0]), "hipEventRecord");
-      tiled.render(p, rgba.data(), c);
-      hip_check(hipSetDevice(0), "hipSetDevice");
-      hip_check(hipEventRecord(t1, tiled.stream[0]), "hipEventRecord");
-      hip_check(hipEventSynchronize(t1), "hipEventSynchronize");
-      float ms = 0.0f;
-      hip_check(hipEventElapsedTime(&ms, t0, t1), "hipEventElapsedTime");
-      (void)hipEventDestroy(t0);
-      (void)hipEventDestroy(t1);
-      st.pixels = c[0], st.hit_pixels = c[1], st.primary_steps = c[2], st.shadow_steps = c[3];
-      st.normal_evals = c[4], st.fractal_bodies = c[5], st.fractal_bailouts = c[6];
-      st.march_steps = c[2] + c[3];
-      st.kernel_ms = ms;  // device 0's view of the whole frame: render, gather, reassembly
-    }
+    check(frm_set_parameters(ctx, &p), ctx, "frm_set_parameters");
+    check(frm_render(ctx, &st), ctx, "frm_render");  // a group: render, gather and reassembly
+    check(frm_read_frame(ctx, rgba.data(), rgba.size()), ctx, "frm_read_frame");
     char name[4096];
     if (strchr(out, '%')) snprintf(name, sizeof(name), out, fr);
     else snprintf(name, sizeof(name), "%s", out);
@@ -338,7 +219,6 @@ int main(int argc, char** argv) {
            cam.pitch, st.kernel_ms, (unsigned long long)st.march_steps, (unsigned long long)st.hit_pixels,
            st.march_steps / (st.kernel_ms * 1e-3) / 1e9);
   }
-  if (ctx) frm_destroy(ctx);
-  else tiled.destroy();
+  frm_destroy(ctx);
   return 0;
 }

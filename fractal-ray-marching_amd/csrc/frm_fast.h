@@ -96,9 +96,10 @@ __device__ __forceinline__ uint32_t bfi_(uint32_t mask, uint32_t a, uint32_t b) 
 }
 
 // sincos_ for |x| <= 2^20 (the branch sincos_ takes there): t = fma(x, 1/pi, K), j = t - K,
-// and j's parity is t's low bit, so the sign (-1)^j of both results is bit 0 of t moved to
-// bit 31 (returned in *sign_out: the caller applies it, sincos_small applies it itself).
-__device__ __forceinline__ void sincos_unsigned(float x, float* s_out, float* c_out, uint32_t* sign_out) {
+// and j's parity is t's low bit, so both results carry the sign (-1)^j = bit 0 of t moved to
+// bit 31. sincos_unsigned returns the unsigned pair and t's encoding (*t_out): the Mandelbulb body
+// applies the signs to its products (sincos_small applies them itself).
+__device__ __forceinline__ void sincos_unsigned(float x, float* s_out, float* c_out, uint32_t* t_out) {
   const float t = fma_(x, kInvPiHi, kRoundK);
   const float j = t - kRoundK;
   float r = fma_(x, kInvPiHi, -j);
@@ -106,12 +107,13 @@ __device__ __forceinline__ void sincos_unsigned(float x, float* s_out, float* c_
   const float u = r * r;
   *s_out = r * sinpi_poly(u);
   *c_out = cospi_poly(u);
-  *sign_out = __float_as_uint(t) << 31;
+  *t_out = __float_as_uint(t);
 }
 __device__ __forceinline__ void sincos_small(float x, float* s_out, float* c_out) {
   float s, c;
-  uint32_t sg;
-  sincos_unsigned(x, &s, &c, &sg);
+  uint32_t t;
+  sincos_unsigned(x, &s, &c, &t);
+  const uint32_t sg = t << 31;
   *s_out = __uint_as_float(__float_as_uint(s) ^ sg);
   *c_out = __uint_as_float(__float_as_uint(c) ^ sg);
 }

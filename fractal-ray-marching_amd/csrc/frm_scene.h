@@ -333,10 +333,17 @@ __device__ __forceinline__ void mb_body_tame(float P, float Pm1, v3 c, float r, 
   float l2 = log2_tame(r);
   dr = fma_(exp2_tame(Pm1 * l2) * P, dr, 1.0f);
   float er = exp2_tame(P * l2);
+  // |theta * P|, |phi * P| <= 9 pi (P in [4, 9]): sincos_'s |x| <= 2^20 branch. The signs
+  // (-1)^j of the two pairs go onto er (a sign flip commutes with the rounding of fma):
+  // x, y take sign(theta pair) ^ sign(phi pair) = bit 31 of (t_theta + t_phi) << 31, z the
+  // theta pair's
   float st, ct, sp, cp;
-  sincos_small(theta * P, &st, &ct);  // |theta * P|, |phi * P| <= 9 pi (P in [4, 9])
-  sincos_small(phi * P, &sp, &cp);
-  z = mk(fma_(er, st * cp, c.x), fma_(er, sp * st, c.y), fma_(er, ct, c.z));
+  uint32_t tt, tp;
+  sincos_unsigned(theta * P, &st, &ct, &tt);
+  sincos_unsigned(phi * P, &sp, &cp, &tp);
+  const float er_xy = __uint_as_float(__float_as_uint(er) ^ ((tt + tp) << 31));
+  const float er_z = __uint_as_float(__float_as_uint(er) ^ (tt << 31));
+  z = mk(fma_(er_xy, st * cp, c.x), fma_(er_xy, sp * st, c.y), fma_(er_z, ct, c.z));
 }
 
 // length() with sqrt_nosmall, exact unless 0 < dot(z,z) < 2^-96.

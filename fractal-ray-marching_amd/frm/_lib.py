@@ -196,6 +196,9 @@ def load():
         pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, restype, argtypes in SIGNATURES:
+        fn = getattr(lib, name, None)
+        if fn is None and os.environ.get("FRM_LIB"):
+            continue  # an A/B build of an earlier ABI (tools/ab_r5.sh) may lack newer entry points
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes

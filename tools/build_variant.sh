@@ -21,5 +21,5 @@ mkdir -p ab
 make -s CSRC="$SRC" OBJDIR=$OBJ EXTRA_HIPFLAGS="$FLAGS" ${SCHEDFLAGS+SCHEDFLAGS="$SCHEDFLAGS"} $OBJ/frm_kernels.o $OBJ/frm_api.o \
   $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ab/$NAME.so $OBJ/frm_kernels.o \
-  $OBJ/frm_api.o $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o -lhiprtc
+  $OBJ/frm_api.o $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o -lhiprtc -lrccl
 echo "ab/$NAME.so"
