@@ -5,8 +5,9 @@
 // path ran (tests/test_gpu_de.py checks the tame path against the oracle).
 //
 // Where the savings come from (hipcc's correctly rounded lowerings, gfx950):
-//  * sqrt: v_sqrt_f32 + a one-ulp correction; the exact lowering also rescales inputs
-//    below 2^-96 (5 instructions) — not needed when x == 0 or x >= 2^-96.
+//  * sqrt: v_rsq_f32 + one residual correction is the correctly rounded sqrt on [2^-96, 2^126]
+//    (exhaustively checked, below), in place of LLVM's v_sqrt + two-sided correction + the rescale
+//    of inputs below 2^-96.
 //  * 1 / b: v_rcp_f32 + one Newton step is RN(1 / b) for every |b| in [2^-125, 2^125]
 //    (checked over all 4.2 G such encodings on gfx950, tools/micro/hw_exact_probe.hip,
 //    profiles/round5/hw_exact.json): the correctly rounded reciprocal in three instructions.
@@ -22,18 +23,22 @@ namespace frm {
 
 #if defined(__HIP_DEVICE_COMPILE__)
 
-// Correctly rounded sqrt, exact for x == +-0, x >= 2^-96, +inf, NaN and x < 0 (all x
-// except subnormals and normals below 2^-96). Mirrors LLVM's expansion minus the rescale
-// and minus its +-0/+inf pass-through: there the one-ulp corrections cannot fire
-// (s = +-0: s_dn is NaN, the s_up residual is +-0; s = +inf: both residuals are NaN).
+// Correctly rounded sqrt for x in [2^-96, 2^126] from the hardware reciprocal square root: s =
+// x y, one residual e = x - s^2 (fma, exact) and s + e (y / 2). Exhaustively checked equal to the
+// correctly rounded sqrtf for every x in [2^-96, 2^128) on gfx950 (tools/micro/hw_exact_probe2.hip,
+// profiles/round5/hw_exact2.json): 5 instructions, one transcendental, no compares or selects
+// (LLVM's correctly rounded expansion: v_sqrt + two neighbour residuals + compares + selects).
+__device__ __forceinline__ float sqrt_rsq(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float s = x * y;
+  return fmaf(fmaf(-s, s, x), 0.5f * y, s);
+}
+
+// Correctly rounded sqrt for x in {+0} U [2^-96, 2^126], negative x and NaN (NaN out, as sqrtf):
+// sqrt_rsq with the zero the reciprocal square root cannot give (rsq(+0) = +inf).
 __device__ __forceinline__ float sqrt_nosmall(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
-  float s_dn = __uint_as_float(__float_as_uint(s) - 1u);
-  float s_up = __uint_as_float(__float_as_uint(s) + 1u);
-  float r_dn = fmaf(-s_dn, s, x);
-  float r_up = fmaf(-s_up, s, x);
-  s = (r_dn <= 0.0f) ? s_dn : s;
-  return (r_up > 0.0f) ? s_up : s;
+  const float s = sqrt_rsq(x);
+  return x == 0.0f ? x : s;
 }
 
 // RN(1 / b) for |b| in [2^-125, 2^125] (exhaustively checked, see above).

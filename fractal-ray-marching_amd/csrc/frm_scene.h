@@ -346,11 +346,13 @@ __device__ __forceinline__ void mb_body_tame(float P, float Pm1, v3 c, float r, 
   z = mk(fma_(er_xy, st * cp, c.x), fma_(er_xy, sp * st, c.y), fma_(er_z, ct, c.z));
 }
 
-// length() with sqrt_nosmall, exact unless 0 < dot(z,z) < 2^-96.
-__device__ __forceinline__ float length_nosmall(v3 a) { return sqrt_nosmall(dot(a, a)); }
-__device__ __forceinline__ bool length_small(v3 a) {
-  float d = dot(a, a);
-  return d > 0.0f && d < 0x1p-96f;
+// length() through sqrt_rsq: exact when dot(a, a) lies in [2^-96, 2^126]. length_wide: whether
+// a lane's dot(a, a) lies outside it (0, tiny, huge, inf, NaN): one integer range test on the
+// encoding (bits - bits(2^-96), unsigned, above the range's width); such a wave takes length().
+__device__ __forceinline__ float length_rsq(v3 a) { return sqrt_rsq(dot(a, a)); }
+__device__ __forceinline__ bool length_wide(v3 a) {
+  constexpr uint32_t kLo = 0x0f800000u, kHi = 0x7e800000u;  // bits of 2^-96, 2^126
+  return __float_as_uint(dot(a, a)) - kLo > kHi - kLo;
 }
 
 #endif
@@ -377,12 +379,13 @@ template <bool HW = false>
 FRM_HD void mb_step(const SceneUniforms& u, v3 c, float r, v3& z, float& dr) {
   mb_step<HW>(u.mb_power, u.mb_power_m1, c, r, z, dr);
 }
-// length(z) for the Mandelbulb magnitude; fast sqrt unless a lane has 0 < |z|^2 < 2^-96.
+// length(z) for the Mandelbulb magnitude; fast sqrt unless a lane's |z|^2 lies outside
+// [2^-96, 2^126] (z = 0 included: the exact sqrtf gives its 0).
 template <bool HW = false>
 FRM_HD float mb_length(v3 z) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (HW) return hw_sqrt(dot(z, z));
-  if (ballot(length_small(z)) == 0) return length_nosmall(z);
+  if (ballot(length_wide(z)) == 0) return length_rsq(z);
 #endif
   return length(z);
 }

@@ -105,8 +105,13 @@ def _tame(rng, n, lo=-60, hi=40, zeros=True):
 def _fast_inputs(name, rng):
     n = 200000
     if name == "sqrt_nosmall":
-        a = np.concatenate([np.exp2(rng.uniform(-96, 128, n)), [0.0, -0.0, np.inf, -1.0, np.nan, 2.0 ** -96,
-                                                                np.finfo(np.float32).max, 1.0]])
+        # the rsq-based fast sqrt (frm_fast.h): +-0, [2^-96, 2^126], negatives and NaN; both ends of
+        # the range and every mantissa boundary around 1 and 4
+        edge = np.array([1.0, 4.0, 2.0 ** -96, 2.0 ** 126], np.float32).view(np.uint32)
+        edge = (edge[:, None] + np.arange(-3, 4)).ravel().astype(np.uint32).view(np.float32).astype(np.float64)
+        edge = edge[(edge >= 2.0 ** -96) & (edge <= 2.0 ** 126)]
+        a = np.concatenate([np.exp2(rng.uniform(-96, 126, n)), edge, [0.0, -0.0, -1.0, -(2.0 ** -100), np.nan,
+                                                                      2.0 ** -96, 2.0 ** 126, 1.0]])
         return "sqrt", a, None
     if name in ("div_tame", "div_tame_nz"):
         a, b = _tame(rng, n), _tame(rng, n, zeros=False)

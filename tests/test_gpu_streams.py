@@ -1,40 +1,65 @@
 """libfrm's render streams and a torch host: frames in flight run on non-blocking
 slot streams by default (FRM_SLOT_STREAMS=cumask opts into CU-masked streams, which HIP creates
 as blocking streams that synchronise with the legacy null stream, torch's default stream). Work a
-torch host puts on its default stream while a second frame is in flight neither waits for the
-render nor disturbs it."""
+torch host puts on its default stream while two frames are in flight neither waits for them nor
+disturbs them, provided the process has hardware queues for its streams: HIP maps streams onto at
+most GPU_MAX_HW_QUEUES queues (4 by default) and work on a shared queue runs in order, so with 4
+the null stream's event can land behind a frame (the scenario therefore runs in a child process
+with its own queue setting, once with 16 queues, asserted, and once with 4, reported)."""
 import hashlib
 import json
 import os
-import time
+import subprocess
+import sys
 
 import pytest
 
-import frm
-
 pytestmark = pytest.mark.gpu
 
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
+
+CHILD = r"""
+import hashlib, json, os, sys, time
+sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "fractal-ray-marching_amd")]
+import torch
+import frm
+g = json.load(open(sys.argv[2]))["HEADLINE_P1"]
+p = frm.Parameters.from_bytes(bytes.fromhex(g["params"]))
+x = torch.ones(1 << 20, device="cuda")
+(x * 2).sum().item()
+with frm.Renderer(max_steps=g["max_steps"], frames_in_flight=2) as r:
+    r.resize(g["width"], g["height"])
+    r.update_parameters_buffer(p)
+    frame_ms = r.render(stats=True)["kernel_ms"]
+    r.render(stats=False)
+    r.render(stats=False)  # two frames in flight on the slot streams
+    ev = torch.cuda.Event()
+    t0 = time.perf_counter()
+    ev.record(torch.cuda.default_stream())
+    ev.synchronize()
+    dt_ms = (time.perf_counter() - t0) * 1e3
+    y = float((x * 3).sum())
+    r.synchronize()
+    ok = hashlib.sha256(r.read_frame().tobytes()).hexdigest() == g["sha256"]
+print(json.dumps({"dt_ms": dt_ms, "frame_ms": frame_ms, "sum_ok": y == 3.0 * (1 << 20), "frame_ok": ok}))
+"""
+
+
+def _run(queues):
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(queues))
+    out = subprocess.run([sys.executable, "-c", CHILD, ROOT, GOLDEN], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def test_torch_default_stream_independent_of_inflight_render(frm_lib):
-    import torch
-    g = json.load(open(GOLDEN))["HEADLINE_P1"]
-    p = frm.Parameters.from_bytes(bytes.fromhex(g["params"]))
-    x = torch.ones(1 << 20, device="cuda")
-    (x * 2).sum().item()  # warm torch's kernels up
-    with frm.Renderer(max_steps=g["max_steps"], frames_in_flight=2) as r:
-        r.resize(g["width"], g["height"])
-        r.update_parameters_buffer(p)
-        frame_ms = r.render(stats=True)["kernel_ms"]
-        r.render(stats=False)  # slot 1
-        r.render(stats=False)  # slot 0 again: two frames in flight on the slot streams
-        t0 = time.perf_counter()
-        y = (x * 3).sum()  # the default (null) stream
-        torch.cuda.current_stream().synchronize()
-        dt_ms = (time.perf_counter() - t0) * 1e3
-        assert float(y) == 3.0 * (1 << 20)
-        r.synchronize()
-        assert hashlib.sha256(r.read_frame().tobytes()).hexdigest() == g["sha256"]
-    # a blocking stream would have held the torch op behind both frames (about 2 x frame_ms)
-    assert dt_ms < 0.5 * frame_ms, (dt_ms, frame_ms)
+    r16 = _run(16)
+    assert r16["sum_ok"] and r16["frame_ok"], r16
+    # an event on the null stream completes at once: it is not ordered after the slot streams (a
+    # blocking slot stream would hold it behind both frames, about 2 x frame_ms)
+    assert r16["dt_ms"] < 0.25 * r16["frame_ms"], r16
+    r4 = _run(4)  # HIP's default queue count: the bytes stay exact whatever the event waits for
+    assert r4["sum_ok"] and r4["frame_ok"], r4
+    print("GPU_MAX_HW_QUEUES=16:", r16, "GPU_MAX_HW_QUEUES=4:", r4)
