@@ -30,6 +30,8 @@ static constexpr uint64_t kSimplePixelsPerCu = 1536;
 // Queue positions a launch may claim beyond its pixels (2 chunks per wave of a grid of up to
 // 2^17 waves); launches are limited to 2^32 - 1 - this many fetch positions.
 static constexpr uint64_t kQueueHeadroom = 1ull << 24;
+// Persistent grid of a single-frame launch on a context with frames in flight (launch()).
+static constexpr int kInflightBlocksPerCu = 12;
 
 // One frame in flight: the device state a render launch owns until it completes. A context
 // has config.frames_in_flight slots and launches round-robin over them, so frame k+1 can
@@ -505,7 +507,15 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   if (kind != kKernelPersistent) sl.order_ready = false;
   const ServiceStream* service = nullptr;
   if (int rc = slot_service(ctx, sl, &service)) return rc;
-  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded, service));
+  // Single-frame persistent launches with frames in flight run a grid of 3 waves per SIMD (12
+  // one-wave workgroups per CU) instead of the occupancy limit (7 for the Mandelbulb): two frames'
+  // grids then share the GPU, each frame's shading and ranking find room beside the next frame's
+  // grid, and one frame's tail runs beside the other's bulk. Measured (profiles/round5/dropin_bpc):
+  // the drop-in loop 9.11-9.18 -> 8.57-8.60 ms (fixed pose), 10.08-10.13 -> 9.29-9.32 (HEADLINE_FLY);
+  // multi-frame launches (one queue for all their frames) keep the full grid (8-way rank share
+  // 1.098 ms/frame full, 1.117 at 12).
+  const int blocks_cap = (a.batch == 1 && ctx->nslots >= 2) ? kInflightBlocksPerCu : 0;
+  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded, service, blocks_cap));
   if (a.key_hist) {
     sl.order_ready = true;
     sl.rank_half ^= 1u;

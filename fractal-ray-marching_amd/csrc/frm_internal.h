@@ -140,8 +140,9 @@ struct ServiceStream {
   hipStream_t svc = nullptr;
   hipEvent_t marched = nullptr, serviced = nullptr;
 };
+// blocks_cap: at most this many persistent workgroups (one wave each) per CU; 0 = the occupancy limit
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
-                         const ReloadedKernels* rk, const ServiceStream* service = nullptr);
+                         const ReloadedKernels* rk, const ServiceStream* service = nullptr, int blocks_cap = 0);
 hipError_t launch_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                        uint32_t flags, hipStream_t stream);
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,

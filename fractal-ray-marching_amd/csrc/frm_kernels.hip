@@ -163,7 +163,7 @@ static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStre
 // on ROCm 7.2 (5 waves/SIMD), the multi-frame one 80 (6 waves/SIMD).
 template <uint32_t FAM, bool ITERS>
 static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStream_t stream,
-                                    const ReloadedKernels* rk, const ServiceStream* service) {
+                                    const ReloadedKernels* rk, const ServiceStream* service, int blocks_cap) {
   // occupancy of each built-in instantiation (per process); reloaded modules query their own
   // (frm_reload.hip)
   static int blocks_per_cu = 0, blocks_per_cu_anim = 0;
@@ -181,6 +181,7 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
     }
   }
   int bpc = rk ? rk->persistent_blocks_per_cu[FAM][ITERS] : (args.anim ? blocks_per_cu_anim : blocks_per_cu);
+  if (blocks_cap > 0 && bpc > blocks_cap) bpc = blocks_cap;
   if (const int v = blocks_override()) bpc = v;
   // every wave starts with one chunk of 64 pixels; never launch more waves than chunks
   uint32_t blocks = (uint32_t)(bpc * cu_count);
@@ -235,10 +236,10 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
 
 template <uint32_t FAM>
 static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
-                                const ReloadedKernels* rk, const ServiceStream* service) {
+                                const ReloadedKernels* rk, const ServiceStream* service, int blocks_cap) {
   if (kind == kKernelPersistent)
-    return args.s.n ? launch_persistent<FAM, true>(args, cu_count, stream, rk, service)
-                    : launch_persistent<FAM, false>(args, cu_count, stream, rk, service);
+    return args.s.n ? launch_persistent<FAM, true>(args, cu_count, stream, rk, service, blocks_cap)
+                    : launch_persistent<FAM, false>(args, cu_count, stream, rk, service, blocks_cap);
   dim3 grid((args.f.width + 15u) / 16u, (args.g.local_rows + 15u) / 16u);
   if (rk) return module_launch(rk->simple[FAM][args.s.n ? 1 : 0], grid, dim3(256), stream, args);
   if (args.s.n)
@@ -249,14 +250,14 @@ static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_
 }
 
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
-                         const ReloadedKernels* rk, const ServiceStream* service) {
+                         const ReloadedKernels* rk, const ServiceStream* service, int blocks_cap) {
   switch (args.s.family) {
-    case kMenger: return launch_family<kMenger>(args, kind, cu_count, stream, rk, service);
-    case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream, rk, service);
-    case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream, rk, service);
-    case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream, rk, service);
-    case kMandelbulbHw: return launch_family<kMandelbulbHw>(args, kind, cu_count, stream, rk, service);
-    default: return launch_family<kSphere>(args, kind, cu_count, stream, rk, service);
+    case kMenger: return launch_family<kMenger>(args, kind, cu_count, stream, rk, service, blocks_cap);
+    case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream, rk, service, blocks_cap);
+    case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream, rk, service, blocks_cap);
+    case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream, rk, service, blocks_cap);
+    case kMandelbulbHw: return launch_family<kMandelbulbHw>(args, kind, cu_count, stream, rk, service, blocks_cap);
+    default: return launch_family<kSphere>(args, kind, cu_count, stream, rk, service, blocks_cap);
   }
 }
 
