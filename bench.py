@@ -130,7 +130,7 @@ def cpu_baseline(params, w, seconds):
             rows, stride, r, dt = sample(n, nthreads)
         steps = int(r["counters"][2]) + int(r["counters"][3])
         text = (f"{len(rows)} evenly spaced rows (one in {stride}) of the {w.width}x{w.height} frame, "
-                f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O2, {nthreads} thread"
+                f"{steps} march steps in {dt:.2f} s; oracle/frm_oracle.c, gcc -O3 -mfma -ffp-contract=off (oracle/Makefile), {nthreads} thread"
                 f"{'s' if nthreads > 1 else ''}")
         return steps / dt / 1e9, text, (len(rows) / w.height) / dt
 
