@@ -81,9 +81,6 @@ struct Slot {
   // `copied` is recorded after the copy, and the slot's next frm_render waits for it before its
   // launch rewrites the framebuffer. The render stream itself goes straight on to the next frame.
   hipStream_t copy_stream = nullptr;
-  // the frame's service kernels' stream (frm_ctx::svc_priority, FRM_SVC_STREAM): shade_pass and
-  // rank_pass leave the slot stream after the march
-  ServiceStream service;
   uint8_t* host_img = nullptr;
   size_t host_cap = 0;
   uint8_t* present_dev = nullptr;  // frm_present_async's blit output (device, context pool), grown on demand
@@ -150,9 +147,6 @@ struct frm_ctx {
   unsigned long long* counters = nullptr;  // FRM_NUM_COUNTERS
   uint32_t service_min = kDefaultServiceMin;
   bool fused_sched = true;  // KernelArgs::key_hist; FRM_SCHED=sort: every launch sorts (experiments)
-  // service streams (experiments, FRM_SVC_STREAM=high|normal): 0 off, 1 default priority,
-  // 2 the device's greatest priority (also for the copy streams)
-  int svc_mode = 0;
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
@@ -357,28 +351,6 @@ hipStream_t own_queue_stream(int device) {
   return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? s : nullptr;
 }
 
-// A non-blocking stream at the device's greatest priority (high) or the default one.
-hipError_t make_stream(hipStream_t* s, bool high) {
-  if (!high) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-  int least = 0, greatest = 0;
-  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-  if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
-}
-
-// The slot's service stream and its two events (created on first use).
-int slot_service(frm_ctx* ctx, Slot& sl, const ServiceStream** out) {
-  *out = nullptr;
-  if (!ctx->svc_mode) return FRM_OK;
-  if (!sl.service.svc) {
-    FRM_HIP(ctx, make_stream(&sl.service.svc, ctx->svc_mode == 2));
-    FRM_HIP(ctx, hipEventCreateWithFlags(&sl.service.marched, hipEventDisableTiming));
-    FRM_HIP(ctx, hipEventCreateWithFlags(&sl.service.serviced, hipEventDisableTiming));
-  }
-  *out = &sl.service;
-  return FRM_OK;
-}
-
 int slot_stream(frm_ctx* ctx, uint32_t i, hipStream_t* out) {
   Slot& sl = ctx->slots[i];
   if (!sl.stream && !(sl.stream = own_queue_stream(ctx->device)))
@@ -505,8 +477,6 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
 #endif
   }
   if (kind != kKernelPersistent) sl.order_ready = false;
-  const ServiceStream* service = nullptr;
-  if (int rc = slot_service(ctx, sl, &service)) return rc;
   // Single-frame persistent launches with frames in flight run a grid of 3 waves per SIMD (12
   // one-wave workgroups per CU) instead of the occupancy limit (7 for the Mandelbulb): two frames'
   // grids then share the GPU, each frame's shading and ranking find room beside the next frame's
@@ -515,7 +485,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   // multi-frame launches (one queue for all their frames) keep the full grid (8-way rank share
   // 1.098 ms/frame full, 1.117 at 12).
   const int blocks_cap = (a.batch == 1 && ctx->nslots >= 2) ? kInflightBlocksPerCu : 0;
-  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded, service, blocks_cap));
+  FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded, blocks_cap));
   if (a.key_hist) {
     sl.order_ready = true;
     sl.rank_half ^= 1u;
@@ -748,7 +718,6 @@ static int create_one(const frm_config* config, int device, frm_ctx** out_ctx) {
   ctx->flags = config->flags;
   ctx->nslots = config->frames_in_flight ? config->frames_in_flight : 1u;
   if (const char* env = getenv("FRM_SCHED")) ctx->fused_sched = strcmp(env, "sort") != 0;
-  if (const char* env = getenv("FRM_SVC_STREAM")) ctx->svc_mode = !strcmp(env, "high") ? 2 : !strcmp(env, "normal") ? 1 : 0;
   if (const char* env = getenv("FRM_SERVICE_MIN")) {
     long v = strtol(env, nullptr, 10);
     if (v >= 1 && v <= 64) ctx->service_min = (uint32_t)v;
@@ -918,12 +887,6 @@ int frm_destroy(frm_ctx* ctx) {
     if (sl.host_img) (void)hipHostFree(sl.host_img);
     if (i > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
     if (sl.copy_stream) (void)hipStreamDestroy(sl.copy_stream);
-    if (sl.service.svc) {
-      (void)hipStreamSynchronize(sl.service.svc);
-      (void)hipStreamDestroy(sl.service.svc);
-      (void)hipEventDestroy(sl.service.marched);
-      (void)hipEventDestroy(sl.service.serviced);
-    }
   }
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
@@ -1072,7 +1035,7 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
 
 // The slot's copy stream, ordered after the slot's last launch (its render).
 static int copy_stream_after_render(frm_ctx* ctx, Slot& sl) {
-  if (!sl.copy_stream) FRM_HIP(ctx, make_stream(&sl.copy_stream, ctx->svc_mode == 2));
+  if (!sl.copy_stream) FRM_HIP(ctx, hipStreamCreateWithFlags(&sl.copy_stream, hipStreamNonBlocking));
   FRM_HIP(ctx, hipStreamWaitEvent(sl.copy_stream, sl.done, 0));
   return FRM_OK;
 }

@@ -133,16 +133,9 @@ void unload_reloaded(ReloadedKernels* rk);
 
 // frm_kernels.hip (rk: a reloaded module's kernels, or nullptr for the built-in ones)
 enum KernelKind : uint32_t { kKernelPersistent = 0, kKernelSimple = 1 };
-// A frame's service kernels (shade_pass, rank_pass) on their own stream: `svc` waits for
-// `marched` (recorded after the march on `stream`), `stream` then waits for `serviced`. NULL svc:
-// everything on `stream`, in order.
-struct ServiceStream {
-  hipStream_t svc = nullptr;
-  hipEvent_t marched = nullptr, serviced = nullptr;
-};
 // blocks_cap: at most this many persistent workgroups (one wave each) per CU; 0 = the occupancy limit
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
-                         const ReloadedKernels* rk, const ServiceStream* service = nullptr, int blocks_cap = 0);
+                         const ReloadedKernels* rk, int blocks_cap = 0);
 hipError_t launch_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                        uint32_t flags, hipStream_t stream);
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,

@@ -163,7 +163,7 @@ static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStre
 // on ROCm 7.2 (5 waves/SIMD), the multi-frame one 80 (6 waves/SIMD).
 template <uint32_t FAM, bool ITERS>
 static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStream_t stream,
-                                    const ReloadedKernels* rk, const ServiceStream* service, int blocks_cap) {
+                                    const ReloadedKernels* rk, int blocks_cap) {
   // occupancy of each built-in instantiation (per process); reloaded modules query their own
   // (frm_reload.hip)
   static int blocks_per_cu = 0, blocks_per_cu_anim = 0;
@@ -191,27 +191,10 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   if (blocks == 0) blocks = 1;
   const uint32_t pixels = args.g.local_rows * args.f.width;
   const uint32_t shade_blocks = (pixels + kShadeBlockPixels - 1u) / kShadeBlockPixels;
-  // the service kernels' stream: `stream` itself, or the caller's service stream after the march
-  hipStream_t sv = stream;
-  auto to_service = [&]() -> hipError_t {
-    if (!service || !service->svc) return hipSuccess;
-    hipError_t e = hipEventRecord(service->marched, stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(service->svc, service->marched, 0);
-    sv = service->svc;
-    return e;
-  };
-  auto from_service = [&]() -> hipError_t {
-    if (sv == stream) return hipSuccess;
-    hipError_t e = hipEventRecord(service->serviced, sv);
-    if (e == hipSuccess) e = hipStreamWaitEvent(stream, service->serviced, 0);
-    return e;
-  };
   if (rk) {
     hipError_t e = module_launch(rk->persistent[FAM][ITERS], dim3(blocks), dim3(kMarchBlock), stream, args);
-    if (e == hipSuccess) e = to_service();
-    if (e == hipSuccess) e = module_launch(rk->shade[FAM], dim3(shade_blocks, args.batch), dim3(256), sv, args);
-    if (e == hipSuccess) e = from_service();
-    return e;
+    if (e != hipSuccess) return e;
+    return module_launch(rk->shade[FAM], dim3(shade_blocks, args.batch), dim3(256), stream, args);
   }
   if constexpr (is_mandelbulb(FAM) && ITERS) {
     if (args.anim) {
@@ -222,24 +205,19 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
   } else {
     hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
   }
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = to_service();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((shade_pass<FAM>), dim3(shade_blocks, args.batch), dim3(256), 0, sv, args);
+  hipLaunchKernelGGL((shade_pass<FAM>), dim3(shade_blocks, args.batch), dim3(256), 0, stream, args);
   if (args.key_hist)  // fused scheduling: the slot's next fetch order
-    hipLaunchKernelGGL(rank_pass, dim3((args.npix + kShadeBlockPixels - 1u) / kShadeBlockPixels), dim3(256), 0, sv,
+    hipLaunchKernelGGL(rank_pass, dim3((args.npix + kShadeBlockPixels - 1u) / kShadeBlockPixels), dim3(256), 0, stream,
                        args.pixel_key, args.npix, args.key_hist, args.order_out);
-  e = hipGetLastError();
-  if (e == hipSuccess) e = from_service();
-  return e;
+  return hipGetLastError();
 }
 
 template <uint32_t FAM>
 static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
-                                const ReloadedKernels* rk, const ServiceStream* service, int blocks_cap) {
+                                const ReloadedKernels* rk, int blocks_cap) {
   if (kind == kKernelPersistent)
-    return args.s.n ? launch_persistent<FAM, true>(args, cu_count, stream, rk, service, blocks_cap)
-                    : launch_persistent<FAM, false>(args, cu_count, stream, rk, service, blocks_cap);
+    return args.s.n ? launch_persistent<FAM, true>(args, cu_count, stream, rk, blocks_cap)
+                    : launch_persistent<FAM, false>(args, cu_count, stream, rk, blocks_cap);
   dim3 grid((args.f.width + 15u) / 16u, (args.g.local_rows + 15u) / 16u);
   if (rk) return module_launch(rk->simple[FAM][args.s.n ? 1 : 0], grid, dim3(256), stream, args);
   if (args.s.n)
@@ -250,14 +228,14 @@ static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_
 }
 
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
-                         const ReloadedKernels* rk, const ServiceStream* service, int blocks_cap) {
+                         const ReloadedKernels* rk, int blocks_cap) {
   switch (args.s.family) {
-    case kMenger: return launch_family<kMenger>(args, kind, cu_count, stream, rk, service, blocks_cap);
-    case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream, rk, service, blocks_cap);
-    case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream, rk, service, blocks_cap);
-    case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream, rk, service, blocks_cap);
-    case kMandelbulbHw: return launch_family<kMandelbulbHw>(args, kind, cu_count, stream, rk, service, blocks_cap);
-    default: return launch_family<kSphere>(args, kind, cu_count, stream, rk, service, blocks_cap);
+    case kMenger: return launch_family<kMenger>(args, kind, cu_count, stream, rk, blocks_cap);
+    case kSierpinski: return launch_family<kSierpinski>(args, kind, cu_count, stream, rk, blocks_cap);
+    case kKoch: return launch_family<kKoch>(args, kind, cu_count, stream, rk, blocks_cap);
+    case kMandelbulb: return launch_family<kMandelbulb>(args, kind, cu_count, stream, rk, blocks_cap);
+    case kMandelbulbHw: return launch_family<kMandelbulbHw>(args, kind, cu_count, stream, rk, blocks_cap);
+    default: return launch_family<kSphere>(args, kind, cu_count, stream, rk, blocks_cap);
   }
 }
 
