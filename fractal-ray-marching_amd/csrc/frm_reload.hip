@@ -67,9 +67,10 @@ int compile_reloaded(const char* dir, int device, ReloadedKernels** out, std::st
   if (colon != std::string::npos) arch.resize(colon);
   // frm.h: next to the sources, in ../include or ../../include of them, or this build's
   // the AOT build's code-generation options for the render kernels (Makefile SCHEDFLAGS: no SLP
-  // vectorisation into packed f32 ops)
+  // vectorisation into packed f32 ops, wave-uniform branches left unstructurized)
   std::vector<std::string> opts = {arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                                   "-fno-slp-vectorize", "-I" + d};
+                                   "-fno-slp-vectorize", "-mllvm", "-structurizecfg-skip-uniform-regions",
+                                   "-I" + d};
   for (const std::string& inc : {d + "/../include", d + "/../../include", std::string(FRM_INCLUDE_DIR)})
     if (!inc.empty() && is_file(inc + "/frm.h")) opts.push_back("-I" + inc);
 
