@@ -207,15 +207,19 @@ FRM_HD float de_koch(const SceneUniforms& u, v3 p) {
 }
 
 // One Mandelbulb loop body (fragment.wgsl:251-267) at magnitude r = length(z) <= bailout:
-// updates z and dr in place. pow(r, y) is exp2(y*log2(r)) (frm semantics), so log2(r)
-// is shared by both pows. P = power, Pm1 = power - 1 (SceneUniforms::mb_power / mb_power_m1, or
-// one frame's of a multi-frame launch with per-frame powers).
+// updates z and dr in place. pow(r, y) is exp2(y*log2(r)) (frm semantics), and the body's
+// second pow, pow(r, P), is pow(r, P - 1) * r (frm v3, DESIGN.md section 2: P >= 4 here, so
+// the identity is exact in real arithmetic for every r >= 0, and the one extra rounding is
+// smaller than the exp2's amplified log2 error it replaces). P = power, Pm1 = power - 1
+// (SceneUniforms::mb_power / mb_power_m1, or one frame's of a multi-frame launch with
+// per-frame powers).
 FRM_HD void mb_body(float P, float Pm1, v3 c, float r, v3& z, float& dr) {
   float theta = acos_(z.z / r);
   float phi = atan2_(z.y, z.x);
   float l2 = log2_(r);
-  dr = fma_(exp2_(Pm1 * l2) * P, dr, 1.0f);
-  float er = exp2_(P * l2);
+  const float pm1 = exp2_(Pm1 * l2);
+  dr = fma_(pm1 * P, dr, 1.0f);
+  float er = pm1 * r;
   float st, ct, sp, cp;
   sincos_(theta * P, &st, &ct);
   sincos_(phi * P, &sp, &cp);
@@ -313,9 +317,9 @@ __device__ __forceinline__ bool lane_in(uint64_t mask) {
 #if defined(__HIP_DEVICE_COMPILE__)
 // Operands of one Mandelbulb body are tame when r = length(z) is in [2^-13, bailout]
 // and every component of z is 0 or has magnitude >= 2^-60: then z.z / r and
-// min/max(|x|,|y|) are tame divisions, log2(r) has a positive normal argument and both
-// exp2 arguments ((P-1)*log2 r, P*log2 r with P in [4, 9], log2 r in [-13, log2 100])
-// lie in [-117, 60], where exp2_tame's result is normal.
+// min/max(|x|,|y|) are tame divisions, log2(r) has a positive normal argument and the
+// exp2 argument (P-1)*log2 r (P in [4, 9], log2 r in [-13, log2 100]) lies in [-104, 54],
+// where exp2_tame's result is normal (and so is its product with r, pow(r, P): >= 2^-117).
 // Branch-free: (bits << 1) - 1 drops the sign and maps +-0 to UINT_MAX, so one unsigned
 // min3 + compare tests "0 or |v| >= 2^-60" for the three components at once (NaN
 // components also pass, but then r is NaN and fails r >= 2^-40).
@@ -331,8 +335,9 @@ __device__ __forceinline__ void mb_body_tame(float P, float Pm1, v3 c, float r, 
   float theta = acos_dev(div_tame_nz(z.z, r));  // acos_dev(-0) == acos_dev(+0)
   float phi = atan2_tame(z.y, z.x);
   float l2 = log2_tame(r);
-  dr = fma_(exp2_tame(Pm1 * l2) * P, dr, 1.0f);
-  float er = exp2_tame(P * l2);
+  const float pm1 = exp2_tame(Pm1 * l2);
+  dr = fma_(pm1 * P, dr, 1.0f);
+  float er = pm1 * r;  // pow(r, P) = pow(r, P - 1) * r (frm v3)
   // |theta * P|, |phi * P| <= 9 pi (P in [4, 9]): sincos_'s |x| <= 2^20 branch. The signs
   // (-1)^j of the two pairs go onto er (a sign flip commutes with the rounding of fma):
   // x, y take sign(theta pair) ^ sign(phi pair) = bit 31 of (t_theta + t_phi) << 31, z the

@@ -64,7 +64,7 @@ static float wclamp(float x, float lo, float hi) { return wmin(wmax(x, lo), hi);
 static float wmix(float a, float b, float t) { return a * (1.0f - t) + b * t; }
 static float wfract(float x) { return x - floorf(x); }
 
-/* ======================= builtins, OM_FRM (frm semantics v2) ========= */
+/* ======================= builtins, OM_FRM (frm semantics v2; v3 in mandelbulb) ========= */
 static const float PI_F = 3.14159274101257324219f;
 static const float HALF_PI_F = 1.57079637050628662109f;
 static const float INV_PI_HI = 0x1.45f306p-2f; /* RN(1/pi) */
@@ -388,8 +388,11 @@ static float mandelbulb(const om_frame* F, vec3 position, om_counts* C) {
     }
     float theta = b_acos(m, current.z / magnitude);
     float phi = b_atan2(m, current.y, current.x);
-    magnitude_derivative = fmaf(b_pow(m, magnitude, power - 1.0f) * power, magnitude_derivative, 1.0f);
-    float exp_magnitude = b_pow(m, magnitude, power);
+    /* fragment.wgsl:254, 257; frm v3: pow(magnitude, power) evaluated as
+       pow(magnitude, power - 1) * magnitude; OM_LIBM keeps the float64 pow */
+    const float pow_m1 = b_pow(m, magnitude, power - 1.0f);
+    magnitude_derivative = fmaf(pow_m1 * power, magnitude_derivative, 1.0f);
+    float exp_magnitude = m == OM_LIBM ? b_pow(m, magnitude, power) : pow_m1 * magnitude;
     float st, ct, sp, cp;
     b_sincos(m, theta * power, &st, &ct);
     b_sincos(m, phi * power, &sp, &cp);
