@@ -30,8 +30,14 @@ static constexpr uint64_t kSimplePixelsPerCu = 1536;
 // Queue positions a launch may claim beyond its pixels (2 chunks per wave of a grid of up to
 // 2^17 waves); launches are limited to 2^32 - 1 - this many fetch positions.
 static constexpr uint64_t kQueueHeadroom = 1ull << 24;
-// Persistent grid of a single-frame launch on a context with frames in flight (launch()).
+// Persistent grid of a single-frame launch on a context with frames in flight (launch()): with 2
+// in flight at any size (two capped grids fill the CUs side by side: the 8K drop-in loop 37.6 ->
+// 36.2 ms/frame), with more only for launches of up to kInflightCapPixels pixels (two 4K frames),
+// since a third capped grid is only partly resident and a large frame's boundary is a small part
+// of its time (C5, 16384^2, 3 in flight: 533-547 ms/frame capped against 489-491 at the
+// occupancy limit; profiles/round5/c5cap, c4cap).
 static constexpr int kInflightBlocksPerCu = 12;
+static constexpr uint64_t kInflightCapPixels = 2ull * 3840u * 2160u;
 
 // One frame in flight: the device state a render launch owns until it completes. A context
 // has config.frames_in_flight slots and launches round-robin over them, so frame k+1 can
@@ -484,7 +490,8 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   // the drop-in loop 9.11-9.18 -> 8.57-8.60 ms (fixed pose), 10.08-10.13 -> 9.29-9.32 (HEADLINE_FLY);
   // multi-frame launches (one queue for all their frames) keep the full grid (8-way rank share
   // 1.098 ms/frame full, 1.117 at 12).
-  const int blocks_cap = (a.batch == 1 && ctx->nslots >= 2) ? kInflightBlocksPerCu : 0;
+  const bool cap = a.batch == 1 && (ctx->nslots == 2 || (ctx->nslots > 2 && a.npix <= kInflightCapPixels));
+  const int blocks_cap = cap ? kInflightBlocksPerCu : 0;
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded, blocks_cap));
   if (a.key_hist) {
     sl.order_ready = true;
