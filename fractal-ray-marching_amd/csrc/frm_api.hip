@@ -38,6 +38,11 @@ static constexpr uint64_t kQueueHeadroom = 1ull << 24;
 // occupancy limit; profiles/round5/c5cap, c4cap).
 static constexpr int kInflightBlocksPerCu = 12;
 static constexpr uint64_t kInflightCapPixels = 2ull * 3840u * 2160u;
+// Single-frame launches with one frame in flight: 7 waves/SIMD (28 one-wave workgroups per CU)
+// rather than the kernel's 8. A lone frame ends with its costliest pixels' marches, which an
+// eighth wave per SIMD slows (render-and-wait loop 9.38 -> 9.51 ms fixed, 12.15 -> 13.19 moving at
+// 8 waves; profiles/round5/ab_w8); multi-frame launches interleave their frames' tails and take 8.
+static constexpr int kLoneFrameBlocksPerCu = 28;
 
 // One frame in flight: the device state a render launch owns until it completes. A context
 // has config.frames_in_flight slots and launches round-robin over them, so frame k+1 can
@@ -484,14 +489,19 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   }
   if (kind != kKernelPersistent) sl.order_ready = false;
   // Single-frame persistent launches with frames in flight run a grid of 3 waves per SIMD (12
-  // one-wave workgroups per CU) instead of the occupancy limit (7 for the Mandelbulb): two frames'
+  // one-wave workgroups per CU) instead of the occupancy limit (8 for the Mandelbulb): two frames'
   // grids then share the GPU, each frame's shading and ranking find room beside the next frame's
   // grid, and one frame's tail runs beside the other's bulk. Measured (profiles/round5/dropin_bpc):
   // the drop-in loop 9.11-9.18 -> 8.57-8.60 ms (fixed pose), 10.08-10.13 -> 9.29-9.32 (HEADLINE_FLY);
   // multi-frame launches (one queue for all their frames) keep the full grid (8-way rank share
   // 1.098 ms/frame full, 1.117 at 12).
-  const bool cap = a.batch == 1 && (ctx->nslots == 2 || (ctx->nslots > 2 && a.npix <= kInflightCapPixels));
-  const int blocks_cap = cap ? kInflightBlocksPerCu : 0;
+  int blocks_cap = 0;
+  if (a.batch == 1) {
+    if (ctx->nslots == 2 || (ctx->nslots > 2 && a.npix <= kInflightCapPixels))
+      blocks_cap = kInflightBlocksPerCu;
+    else if (ctx->nslots == 1)
+      blocks_cap = kLoneFrameBlocksPerCu;
+  }
   FRM_HIP(ctx, launch_render(a, kind, ctx->cu_count, s, ctx->reloaded, blocks_cap));
   if (a.key_hist) {
     sl.order_ready = true;
