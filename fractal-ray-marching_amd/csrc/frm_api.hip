@@ -30,14 +30,14 @@ static constexpr uint64_t kSimplePixelsPerCu = 1536;
 // Queue positions a launch may claim beyond its pixels (2 chunks per wave of a grid of up to
 // 2^17 waves); launches are limited to 2^32 - 1 - this many fetch positions.
 static constexpr uint64_t kQueueHeadroom = 1ull << 24;
-// Persistent grid of a single-frame launch on a context with frames in flight (launch()): with 2
-// in flight at any size (two capped grids fill the CUs side by side: the 8K drop-in loop 37.6 ->
-// 36.2 ms/frame), with more only for launches of up to kInflightCapPixels pixels (two 4K frames),
-// since a third capped grid is only partly resident and a large frame's boundary is a small part
-// of its time (C5, 16384^2, 3 in flight: 533-547 ms/frame capped against 489-491 at the
-// occupancy limit; profiles/round5/c5cap, c4cap).
+// Persistent grid of a single-frame launch on a context with frames in flight (launch()), for
+// launches of up to kInflightCapPixels pixels (four 4K frames: 8K): the capped grids of two frames
+// fill the CUs side by side (8K drop-in loop 37.6 -> 36.2 ms/frame). A larger frame's boundary is
+// a small part of its time and the cap costs more than it gains (C5, 16384^2: 3 in flight 533-547
+// ms/frame capped against 489-491 at the occupancy limit, 2 in flight 578 against 511;
+// profiles/round5/c5cap, c4cap, final/configs).
 static constexpr int kInflightBlocksPerCu = 12;
-static constexpr uint64_t kInflightCapPixels = 2ull * 3840u * 2160u;
+static constexpr uint64_t kInflightCapPixels = 4ull * 3840u * 2160u;
 // Single-frame launches with one frame in flight: 7 waves/SIMD (28 one-wave workgroups per CU)
 // rather than the kernel's 8. A lone frame ends with its costliest pixels' marches, which an
 // eighth wave per SIMD slows (render-and-wait loop 9.38 -> 9.51 ms fixed, 12.15 -> 13.19 moving at
@@ -497,7 +497,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   // 1.098 ms/frame full, 1.117 at 12).
   int blocks_cap = 0;
   if (a.batch == 1) {
-    if (ctx->nslots == 2 || (ctx->nslots > 2 && a.npix <= kInflightCapPixels))
+    if (ctx->nslots >= 2 && a.npix <= kInflightCapPixels)
       blocks_cap = kInflightBlocksPerCu;
     else if (ctx->nslots == 1)
       blocks_cap = kLoneFrameBlocksPerCu;
