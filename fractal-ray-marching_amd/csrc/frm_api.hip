@@ -36,12 +36,16 @@ static constexpr uint64_t kQueueHeadroom = 1ull << 24;
 // a small part of its time and the cap costs more than it gains (C5, 16384^2: 3 in flight 533-547
 // ms/frame capped against 489-491 at the occupancy limit, 2 in flight 578 against 511;
 // profiles/round5/c5cap, c4cap, final/configs).
-static constexpr int kInflightBlocksPerCu = 12;
+// 16 = half the 8-wave kernel's occupancy (sweep 12/14/16/32 on the drop-in loop: 8.22 / 8.03 /
+// 7.90 / 8.55 ms fixed, 8.96 / 8.82 / 8.71 / 9.87 moving; profiles/round5/dropin_bpc8; with the
+// round-5 7-wave kernel 12 was best, profiles/round5/dropin_bpc).
+static constexpr int kInflightBlocksPerCu = 16;
 static constexpr uint64_t kInflightCapPixels = 4ull * 3840u * 2160u;
 // Single-frame launches with one frame in flight: 7 waves/SIMD (28 one-wave workgroups per CU)
 // rather than the kernel's 8. A lone frame ends with its costliest pixels' marches, which an
-// eighth wave per SIMD slows (render-and-wait loop 9.38 -> 9.51 ms fixed, 12.15 -> 13.19 moving at
-// 8 waves; profiles/round5/ab_w8); multi-frame launches interleave their frames' tails and take 8.
+// eighth wave per SIMD slows when they were not fetched first (render-and-wait loop, moving camera:
+// 12.85-12.91 ms at 28 per CU, 13.11-13.29 at 32; fixed pose 9.55-9.60 against 9.38-9.46;
+// profiles/round5/dropin_bpc8); multi-frame launches interleave their frames' tails and take 8.
 static constexpr int kLoneFrameBlocksPerCu = 28;
 
 // One frame in flight: the device state a render launch owns until it completes. A context
@@ -488,7 +492,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
 #endif
   }
   if (kind != kKernelPersistent) sl.order_ready = false;
-  // Single-frame persistent launches with frames in flight run a grid of 3 waves per SIMD (12
+  // Single-frame persistent launches with frames in flight run a grid of 4 waves per SIMD (16
   // one-wave workgroups per CU) instead of the occupancy limit (8 for the Mandelbulb): two frames'
   // grids then share the GPU, each frame's shading and ranking find room beside the next frame's
   // grid, and one frame's tail runs beside the other's bulk. Measured (profiles/round5/dropin_bpc):
