@@ -34,11 +34,15 @@ __device__ __forceinline__ float sqrt_rsq(float x) {
   return fmaf(fmaf(-s, s, x), 0.5f * y, s);
 }
 
-// Correctly rounded sqrt for x in {+0} U [2^-96, 2^126], negative x and NaN (NaN out, as sqrtf):
-// sqrt_rsq with the zero the reciprocal square root cannot give (rsq(+0) = +inf).
+// Correctly rounded sqrt for x in {+-0} U [2^-96, 2^126], x <= -2^-126 and NaN (NaN out, as
+// sqrtf): sqrt_rsq with the reciprocal square root taken of x + 2^-126, which is x itself on that
+// domain except at +-0 (2^-126 is below half an ulp of 2^-96), where it makes the reciprocal finite
+// (instead of rsq(0) = inf), so that s = x * y is the signed zero sqrt(+-0) is and the correction
+// keeps it. One add instead of a compare and a select.
 __device__ __forceinline__ float sqrt_nosmall(float x) {
-  const float s = sqrt_rsq(x);
-  return x == 0.0f ? x : s;
+  const float y = __builtin_amdgcn_rsqf(x + 0x1p-126f);
+  const float s = x * y;
+  return fmaf(fmaf(-s, s, x), 0.5f * y, s);
 }
 
 // RN(1 / b) for |b| in [2^-125, 2^125] (exhaustively checked, see above).
