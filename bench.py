@@ -150,7 +150,7 @@ def cpu_baseline(params, w, seconds):
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def pmc_summary(workload, world):
+def pmc_summary(workload, world, math="exact"):
     """Hardware counters of the render kernels from the committed rocprofv3 --pmc passes of
     this workload (tools/pmc.sh + tools/pmc_summary.py: one counter group per pass; FETCH_SIZE
     doubled and KiB -> B per MI355X_MICROARCH.md): march_persistent (the dominant kernel:
@@ -159,12 +159,14 @@ def pmc_summary(workload, world):
     PMC collection needs its own profiler passes (they serialise the kernels), so bench.py
     reports the committed measurement and names it, newest round first, and only when the
     summary's recorded source hash equals the hash of the kernel sources being run
-    (frm.provenance): counters of an older kernel are reported as stale, never as current."""
+    (frm.provenance): counters of an older kernel are reported as stale, never as current.
+    --math hw runs another kernel (the FRM_FLAG_HW_MATH instantiation): its counters are keyed
+    pmc_<workload>_hw_<...>.json and are null unless such a pass is committed."""
     from frm import provenance
 
     cur = provenance.source_sha256()
     stale = None
-    tag = workload if world == 1 else f"{workload}_share{world}"
+    tag = (workload if world == 1 else f"{workload}_share{world}") + ("_hw" if math == "hw" else "")
     for rnd in sorted((d for d in os.listdir(os.path.join(ROOT, "profiles")) if d.startswith("round")),
                       key=lambda d: int(d[5:]) if d[5:].isdigit() else -1, reverse=True):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_march.json")
@@ -638,7 +640,7 @@ def main():
         # rank's frame) and the device time per frame
         wom_per_frame = st["wom_ops"] / args.steps / (world if split == 1 else 1)
         achieved = st["wom_ops"] / args.steps / world / frame_s / 1e12  # per GPU
-        pmc = pmc_summary(args.workload, world) or {}
+        pmc = pmc_summary(args.workload, world, args.math) or {}
         out = {
             "metric": METRIC,
             "value": steps_total / elapsed / 1e9,

@@ -811,7 +811,13 @@ static int create_group(const frm_config* config, frm_ctx** out_ctx) {
   G->rccl = n > 1 && distinct && !(gather && strcmp(gather, "copy") == 0);
   hipError_t e = hipSuccess;
   for (uint32_t r = 1; r < n && rc == FRM_OK; ++r) {
-    if ((rc = create_one(config, config->devices[r], &G->sub[r]))) break;
+    if ((rc = create_one(config, config->devices[r], &G->sub[r]))) {
+      // the member's message (create_one left it in g_error) onto the group context, whose error
+      // the failure path below reports
+      const std::string why = g_error;
+      rc = fail(ctx, rc, "devices[%u] = %d: %s", r, config->devices[r], why.c_str());
+      break;
+    }
     G->sub[r]->bands_only = true;
   }
   for (uint32_t r = 0; r < n && rc == FRM_OK; ++r) {

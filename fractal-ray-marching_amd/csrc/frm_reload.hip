@@ -13,10 +13,15 @@
 #include <stdio.h>
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "frm_internal.h"
+
+#if !defined(FRM_RELOAD_MLLVM) || !defined(FRM_RELOAD_MARCH_WAVES)
+#error "built by the Makefile, which passes the render kernels' code-generation options (SCHED_MLLVM, MARCH_WAVES)"
+#endif
 
 #ifndef FRM_INCLUDE_DIR  // this package's include/ (frm.h), set by the Makefile
 #define FRM_INCLUDE_DIR ""
@@ -65,12 +70,25 @@ int compile_reloaded(const char* dir, int device, ReloadedKernels** out, std::st
   std::string arch = std::string("--offload-arch=") + prop.gcnArchName;
   const size_t colon = arch.find(':');  // "gfx950:sramecc+:xnack-" -> "gfx950"
   if (colon != std::string::npos) arch.resize(colon);
-  // frm.h: next to the sources, in ../include or ../../include of them, or this build's
-  // the AOT build's code-generation options for the render kernels (Makefile SCHEDFLAGS: no SLP
-  // vectorisation into packed f32 ops, wave-uniform branches left unstructurized)
+  // the AOT build's code-generation options for the render kernels, passed in by the Makefile from
+  // the variables that build frm_kernels.o (SCHED_MLLVM, MARCH_WAVES): no SLP vectorisation into
+  // packed f32 ops, the register-pressure trackers, wave-uniform branches left unstructurized, and
+  // the march kernel's waves per SIMD, so a reloaded kernel has the built-in one's occupancy
   std::vector<std::string> opts = {arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                                   "-fno-slp-vectorize", "-mllvm", "-structurizecfg-skip-uniform-regions",
-                                   "-I" + d};
+                                   "-fno-slp-vectorize",
+                                   "-DFRM_MARCH_WAVES_PER_SIMD=" + std::to_string(FRM_RELOAD_MARCH_WAVES), "-I" + d};
+  {
+    const std::string mllvm(FRM_RELOAD_MLLVM);
+    for (size_t i = 0; i < mllvm.size();) {
+      const size_t j = std::min(mllvm.find(' ', i), mllvm.size());
+      if (j > i) {
+        opts.push_back("-mllvm");
+        opts.push_back(mllvm.substr(i, j - i));
+      }
+      i = j + 1;
+    }
+  }
+  // frm.h: next to the sources, in ../include or ../../include of them, or this build's
   for (const std::string& inc : {d + "/../include", d + "/../../include", std::string(FRM_INCLUDE_DIR)})
     if (!inc.empty() && is_file(inc + "/frm.h")) opts.push_back("-I" + inc);
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU step: run the given steps in order, each under its own time limit; stop at the
+# GPU session steps: run the given steps in order, each under its own time limit; stop at the
 # first step that ends in anything but success or ordinary test failures (rc 0/1/3).
 # usage: tools/gpu_r5_step.sh 'SECONDS|NAME|COMMAND' ...
 mkdir -p gpurun_out
