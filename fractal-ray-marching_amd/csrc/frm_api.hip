@@ -11,8 +11,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+
 #include <new>
 #include <string>
+#include <vector>
 
 #include "frm.h"
 #include "frm_internal.h"
@@ -132,6 +135,52 @@ struct Group {
   GroupSlot slots[FRM_MAX_FRAMES_IN_FLIGHT];
 };
 
+// The resident frame ring of a context (frm_internal.h RingArgs; resident_render below).
+struct Ring {
+  uint32_t slots = 0;         // R (2 or 4); 0: never set up
+  RingHost* host = nullptr;   // pinned, coherent
+  RingDev* dev = nullptr;
+  // buffers of the ring's frame size (R frames each): records, framebuffers, fetch orders, cost keys,
+  // and the scheduling scratch of its first orders
+  uint8_t* records = nullptr;
+  uint32_t* out = nullptr;
+  uint32_t* order = nullptr;
+  uint8_t* keys = nullptr;
+  uint32_t* iota = nullptr;
+  uint8_t* keys_sorted = nullptr;
+  void* sched_temp = nullptr;
+  size_t sched_temp_bytes = 0;
+  size_t cap = 0;             // pixels per frame the buffers hold
+  bool keys_valid = false;    // keys hold a frame of keys_w x keys_h
+  uint32_t keys_w = 0, keys_h = 0;
+  // zero-copy readback: two pinned host images per slot (frame g: image (g - 1) / R & 1 of its slot),
+  // each the frame it holds (or will hold) and the ticket handed out for it
+  uint32_t* img[kRingSlots][2] = {};
+  size_t img_cap = 0;
+  uint32_t img_seq[kRingSlots][2] = {};
+  uint64_t img_ticket[kRingSlots][2] = {};
+  size_t img_bytes[kRingSlots][2] = {};
+  bool zero_copy = false;     // frm_read_frame_async has been called: frames carry a host image
+  // images replaced by larger ones (a resize) while a ticket still named them: kept until destroy
+  struct Retired {
+    uint64_t ticket;
+    uint32_t* img;
+    uint32_t seq, slot;
+    size_t bytes;
+  };
+  std::vector<Retired> retired;
+  // the generation the ring is set up for (a frame with other scene uniforms, size, aspect or step
+  // cap needs another grid and a fresh ring)
+  bool gen_valid = false;
+  SceneUniforms su{};
+  uint32_t w = 0, h = 0, max_steps = 0;
+  float aspect[2] = {0.f, 0.f};
+  uint32_t next_seq = 1;      // seq of the next posted frame
+  uint32_t last_seq = 0;      // the last posted frame
+  uint32_t grid_id = 0;       // the last launched grid (0: none yet)
+  uint32_t service_waves = 128;
+};
+
 struct frm_ctx {
   int device = 0;
   Group* group = nullptr;   // a group context (frm_config.device_count >= 1)
@@ -165,6 +214,9 @@ struct frm_ctx {
   frm_parameters params{};
   bool has_params = false;
   SceneUniforms scene{};
+  Ring ring;
+  bool ring_enabled = true;  // FRM_RING=0: every frm_render launches its own grid (A/B)
+  bool last_is_ring = false; // the last frm_render posted a ring frame (ring.last_seq)
   std::string error;
 };
 
@@ -664,6 +716,297 @@ int group_render(frm_ctx* ctx, frm_stats* stats) {
   return FRM_OK;
 }
 
+// ---- resident frame ring --------------------------------------------------------------------
+// Single-frame frm_render calls without stats on a context with frames in flight post their frames
+// to the context's ring (frm_internal.h RingArgs) instead of launching a grid each: one persistent
+// grid marches the posted frames in order (a wave moves on to the next frame when one's queue
+// drains, as a multi-frame launch interleaves its frames) and its service waves shade, rank and
+// publish each frame as its last pixel finishes, so a frame's tail overlaps the next frame's bulk as
+// it does inside frm_render_bands_batch. The grid lives as long as frames keep arriving: a march wave
+// that finds nothing left closes it (the last frame it serves is then fixed), and the host launches
+// the next grid when it sees the closed flag after posting (the post and the flag are ordered by
+// sequentially consistent accesses on both sides, so a frame is either seen by the closing grid or
+// served by the next one). frm_read_frame_async tickets of ring frames are zero-copy: the shading also
+// writes the frame into a pinned host image. Anything else on the context first drains the ring
+// (ring_quiesce).
+
+uint32_t ring_size(const frm_ctx* ctx) { return ctx->nslots >= 3 ? 4u : 2u; }
+
+// Whether frm_render(ctx, NULL) goes through the ring.
+bool ring_eligible(const frm_ctx* ctx) {
+  if (!ctx->ring_enabled || ctx->group || ctx->bands_only || ctx->reloaded || ctx->nslots < 2) return false;
+  const uint64_t npix = (uint64_t)ctx->width * ctx->height;
+  if (kernel_for(ctx, npix) != kKernelPersistent || npix > (1ull << 28)) return false;
+  // a ring's service waves give up after kRingWatchdogTicks (2 s) without progress: keep the
+  // costliest possible pixel (2 marches of max_steps DEs of N + 1 bodies) well inside that
+  const uint64_t trips = (ctx->scene.family == kSphere ? 0u : (uint64_t)ctx->scene.n) + 2u;
+  return 2ull * ctx->max_steps * trips <= (1ull << 21);
+}
+
+bool ring_same_gen(const frm_ctx* ctx) {
+  const Ring& R = ctx->ring;
+  if (!R.gen_valid || R.w != ctx->width || R.h != ctx->height || R.max_steps != ctx->max_steps ||
+      R.aspect[0] != ctx->params.aspect_scale[0] || R.aspect[1] != ctx->params.aspect_scale[1] ||
+      R.slots != ring_size(ctx))
+    return false;
+  SceneUniforms a = R.su, b = ctx->scene;
+  if (is_mandelbulb(a.family)) {  // ring frames carry their own power (march_persistent<..., ANIM, RES>)
+    a.mb_power = b.mb_power = 0.f;
+    a.mb_power_m1 = b.mb_power_m1 = 0.f;
+  }
+  return memcmp(&a, &b, sizeof(a)) == 0;
+}
+
+// Waits (host) until ring frame `seq` (slot s) is done. A grid that ended without it (a service
+// wave's watchdog) is reported instead of waited for.
+int ring_wait(frm_ctx* ctx, uint32_t s, uint32_t seq) {
+  Ring& R = ctx->ring;
+  for (uint64_t spin = 1;; ++spin) {
+    if (__atomic_load_n(&R.host->done[s][0], __ATOMIC_ACQUIRE) >= seq) return FRM_OK;
+    if ((spin & 255u) == 0) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(&R.host->done[s][0], __ATOMIC_ACQUIRE) >= seq) return FRM_OK;
+        return fail(ctx, FRM_ERR_HIP, "resident frame ring: frame %u never completed (its grid ended)", seq);
+      }
+      if (e != hipErrorNotReady) return hip_fail(ctx, e, "hipStreamQuery");
+      sched_yield();
+    }
+  }
+}
+
+// Every posted ring frame done and the ring's grids ended (the last one closes once nothing is
+// left to claim). The context stream is then idle.
+int ring_quiesce(frm_ctx* ctx) {
+  Ring& R = ctx->ring;
+  if (!R.grid_id) return FRM_OK;
+  const uint32_t first = R.last_seq >= R.slots ? R.last_seq - R.slots + 1u : 1u;
+  for (uint32_t q = first; q <= R.last_seq && q >= 1u; ++q)
+    if (int rc = ring_wait(ctx, (q - 1u) & (R.slots - 1u), q)) return rc;
+  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return FRM_OK;
+}
+
+void ring_free_buffers(Ring& R) {
+  for (void* b : {(void*)R.records, (void*)R.out, (void*)R.order, (void*)R.keys, (void*)R.iota, (void*)R.keys_sorted,
+                  R.sched_temp})
+    if (b) (void)hipFree(b);
+  R.records = nullptr;
+  R.out = R.order = R.iota = nullptr;
+  R.keys = R.keys_sorted = nullptr;
+  R.sched_temp = nullptr;
+  R.cap = 0;
+  R.keys_valid = false;
+}
+
+void ring_free_images(Ring& R) {
+  for (uint32_t s = 0; s < kRingSlots; ++s)
+    for (uint32_t par = 0; par < 2; ++par) {
+      uint32_t*& p = R.img[s][par];
+      if (p && R.img_ticket[s][par])  // a ticket still names it (frm_frame_pixels)
+        R.retired.push_back({R.img_ticket[s][par], p, R.img_seq[s][par], s, R.img_bytes[s][par]});
+      else if (p)
+        (void)hipHostFree(p);
+      p = nullptr;
+    }
+  memset(R.img_seq, 0, sizeof(R.img_seq));
+  memset(R.img_ticket, 0, sizeof(R.img_ticket));
+  R.img_cap = 0;
+}
+
+// A fresh ring for the context's current size, scene and step cap, after every earlier ring frame
+// (synchronous: rare, between generations). Each slot's counters carry the epoch of the first new
+// frame that will use it; each slot's first fetch order comes from the ring's cost keys of a frame
+// of the same size (row-major without).
+int ring_setup(frm_ctx* ctx) {
+  Ring& R = ctx->ring;
+  int rc = ring_quiesce(ctx);
+  if (rc) return rc;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (!R.host) {
+    FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&R.host), sizeof(RingHost), hipHostMallocCoherent));
+    memset(R.host, 0, sizeof(RingHost));
+  }
+  if (!R.dev) FRM_HIP(ctx, hipMalloc(&R.dev, sizeof(RingDev)));
+  const uint32_t slots = ring_size(ctx);
+  const size_t npix = (size_t)ctx->width * ctx->height;
+  if (npix > R.cap || slots != R.slots) {
+    ring_free_buffers(R);
+    const size_t n = npix * slots;
+    FRM_HIP(ctx, hipMalloc(&R.records, n * kRecordBytes));
+    FRM_HIP(ctx, hipMalloc(&R.out, n * 4u));
+    FRM_HIP(ctx, hipMalloc(&R.order, n * 4u));
+    FRM_HIP(ctx, hipMalloc(&R.keys, n));
+    FRM_HIP(ctx, hipMalloc(&R.iota, npix * 4u));
+    FRM_HIP(ctx, hipMalloc(&R.keys_sorted, npix));
+    R.sched_temp_bytes = schedule_temp_bytes((uint32_t)npix);
+    FRM_HIP(ctx, hipMalloc(&R.sched_temp, R.sched_temp_bytes ? R.sched_temp_bytes : 16));
+    R.cap = npix;
+  }
+  if (slots != R.slots) ring_free_images(R);
+  R.slots = slots;
+  // slot s's next frame: the first seq >= next_seq with (seq - 1) % R == s
+  const uint32_t k0 = R.next_seq;
+  RingDev* img = new (std::nothrow) RingDev();
+  if (!img) return fail(ctx, FRM_ERR_OUT_OF_MEMORY, "host allocation failed");
+  img->base = k0;
+  for (uint32_t s = 0; s < kRingSlots; ++s) {
+    const uint32_t seq = k0 + ((s + slots - ((k0 - 1u) & (slots - 1u))) & (slots - 1u));
+    const unsigned long long ep = (unsigned long long)seq << 32;
+    RingSlotCtl& c = img->slot[s];
+    for (uint32_t x = 0; x <= kQueueParts; ++x) c.queue[x * (kQueuePartWords / 2u)] = ep;
+    c.pix_done[0] = c.shade_next[0] = c.shade_done[0] = c.rank_next[0] = c.rank_done[0] = ep;
+    const uint32_t prev = seq > slots ? seq - slots : 0u;
+    c.done_seq[0] = prev;
+    if (s < slots) __atomic_store_n(&R.host->done[s][0], prev, __ATOMIC_RELAXED);
+  }
+  const hipError_t e = hipMemcpy(R.dev, img, sizeof(RingDev), hipMemcpyHostToDevice);
+  delete img;
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpy(ring state)");
+  const bool history = R.keys_valid && R.keys_w == ctx->width && R.keys_h == ctx->height;
+  FRM_HIP(ctx, fill_iota(R.iota, (uint32_t)npix, ctx->stream));
+  for (uint32_t s = 0; s < slots; ++s)
+    FRM_HIP(ctx, schedule_pixels((uint32_t)npix, history, R.keys + s * npix, R.keys_sorted, R.iota, R.order + s * npix,
+                                 R.sched_temp, R.sched_temp_bytes, ctx->stream));
+  FRM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  R.keys_valid = true;  // every ring frame's shading writes them
+  R.keys_w = ctx->width;
+  R.keys_h = ctx->height;
+  R.gen_valid = true;
+  R.su = ctx->scene;
+  R.w = ctx->width;
+  R.h = ctx->height;
+  R.max_steps = ctx->max_steps;
+  R.aspect[0] = ctx->params.aspect_scale[0];
+  R.aspect[1] = ctx->params.aspect_scale[1];
+  return FRM_OK;
+}
+
+// A new grid for the ring, serving frames from `first` on (or from where its predecessor stopped).
+int ring_launch(frm_ctx* ctx, uint32_t first) {
+  Ring& R = ctx->ring;
+  const uint32_t id = R.grid_id + 1u;
+  __atomic_store_n(&R.host->grid_stop[id % kRingGridIds][0], 0xFFFFFFFFu, __ATOMIC_SEQ_CST);
+  FRM_HIP(ctx, hipMemsetAsync(&R.dev->grid, 0, sizeof(RingGridCtl), ctx->stream));
+  KernelArgs a = make_args(ctx, nullptr, ctx->counters, ctx->height, 0, 1, ctx->height);
+  const size_t n = R.cap * R.slots;
+  a.geom = reinterpret_cast<ShadeGeom*>(R.records);
+  a.tails = reinterpret_cast<ShadeTail*>(R.records + n * sizeof(ShadeGeom));
+  a.ring.host = R.host;
+  a.ring.dev = R.dev;
+  a.ring.slots = R.slots;
+  a.ring.grid_id = id;
+  a.ring.first_seq = first;
+  a.ring.service_waves = R.service_waves;
+  a.ring.out = R.out;
+  a.ring.order = R.order;
+  a.ring.keys = R.keys;
+  int blocks = 0;
+  FRM_HIP(ctx, launch_ring(a, ctx->cu_count, ctx->stream, &blocks));
+  R.grid_id = id;
+  return FRM_OK;
+}
+
+// frm_render(ctx, NULL) through the ring: post the frame, launching a grid if none will take it.
+int ring_render(frm_ctx* ctx) {
+  Ring& R = ctx->ring;
+  int rc = FRM_OK;
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (!ring_same_gen(ctx) && (rc = ring_setup(ctx))) return rc;
+  const uint32_t k = R.next_seq;
+  const uint32_t s = (k - 1u) & (R.slots - 1u);
+  if ((rc = ring_wait(ctx, s, k > R.slots ? k - R.slots : 0u))) return rc;  // the slot's last frame
+  FrameUniforms fu;
+  compute_frame_uniforms(ctx->params, ctx->width, ctx->height, ctx->max_steps, &fu);
+  RingFrame& F = R.host->frames[s];
+  memcpy(F.row, fu.row, sizeof(F.row));
+  F.ox = fu.origin.x;
+  F.oy = fu.origin.y;
+  F.oz = fu.origin.z;
+  F.mb_power = ctx->scene.mb_power;
+  F.seq = k;
+  uint32_t* img = nullptr;
+  if (R.zero_copy) {
+    const size_t bytes = (size_t)ctx->width * ctx->height * 4u;
+    if (bytes > R.img_cap) {  // images of another size: none of them is pending (ring_setup drained)
+      ring_free_images(R);
+      R.img_cap = bytes + bytes / 4u;  // headroom for the reference's +-1 render-texture steps
+    }
+    const uint32_t par = ((k - 1u) / R.slots) & 1u;
+    if (!R.img[s][par])
+      FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&R.img[s][par]), R.img_cap, hipHostMallocCoherent));
+    img = R.img[s][par];
+    R.img_seq[s][par] = k;
+    R.img_ticket[s][par] = 0;  // its earlier frame's ticket expires
+    R.img_bytes[s][par] = bytes;
+  }
+  F.host_img = img;
+  __atomic_store_n(&R.host->posted, k, __ATOMIC_SEQ_CST);  // after the frame's data
+  // the running grid takes the frame unless it has closed (then it may or may not have seen it: a
+  // new grid starts where the closed one stopped)
+  if (R.grid_id == 0 || __atomic_load_n(&R.host->closed, __ATOMIC_SEQ_CST) == R.grid_id)
+    if ((rc = ring_launch(ctx, k))) return rc;
+  R.next_seq = k + 1u;
+  R.last_seq = k;
+  ctx->last_is_ring = true;
+  ctx->render_params = ctx->params;
+  ctx->render_scene = ctx->scene;
+  return FRM_OK;
+}
+
+// The last frm_render was a ring frame: drain the ring and copy that frame into slot 0's framebuffer,
+// so the single-frame paths (frm_read_frame, frm_present, their async forms) see it as before.
+int ring_materialize(frm_ctx* ctx) {
+  if (!ctx->last_is_ring) return FRM_OK;
+  Ring& R = ctx->ring;
+  int rc = ring_quiesce(ctx);
+  if (rc) return rc;
+  Slot& sl = ctx->slots[0];
+  const size_t bytes = (size_t)ctx->width * ctx->height * 4u;
+  if ((rc = select_fb(ctx, sl, sl.fb_idx)) || (rc = ensure_fb(ctx, sl, bytes + bytes / 4u))) return rc;
+  const uint32_t s = (R.last_seq - 1u) & (R.slots - 1u);
+  FRM_HIP(ctx, hipMemcpyAsync(sl.fb, R.out + (size_t)s * R.w * R.h, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  FRM_HIP(ctx, hipEventRecord(sl.done, ctx->stream));
+  sl.pending = true;
+  sl.last_stream = ctx->stream;
+  sl.seq = ++ctx->launch_seq;
+  ctx->last_slot = 0;
+  ctx->render_seq = sl.seq;
+  ctx->last_is_ring = false;
+  return FRM_OK;
+}
+
+// frm_read_frame_async of a ring frame: a ticket for its zero-copy image. The frame before the first
+// such call was posted without an image: it is waited for and copied once, and from then on every
+// ring frame carries one.
+int ring_read_async(frm_ctx* ctx, uint64_t* out_ticket) {
+  Ring& R = ctx->ring;
+  R.zero_copy = true;
+  const uint32_t k = R.last_seq, s = (k - 1u) & (R.slots - 1u), par = ((k - 1u) / R.slots) & 1u;
+  const size_t bytes = (size_t)R.w * R.h * 4u;
+  if (!(R.img[s][par] && R.img_seq[s][par] == k)) {
+    int rc = ring_quiesce(ctx);
+    if (rc) return rc;
+    if (bytes > R.img_cap) {
+      ring_free_images(R);
+      R.img_cap = bytes + bytes / 4u;
+    }
+    if (!R.img[s][par])
+      FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&R.img[s][par]), R.img_cap, hipHostMallocCoherent));
+    FRM_HIP(ctx, hipMemcpy(R.img[s][par], R.out + (size_t)s * R.w * R.h, bytes, hipMemcpyDeviceToHost));
+    R.img_seq[s][par] = k;
+    R.img_bytes[s][par] = bytes;
+  }
+  R.img_ticket[s][par] = *out_ticket = ++ctx->ticket_seq;
+  return FRM_OK;
+}
+
+// Drains the ring before anything that is not a ring frame uses the context.
+int ring_leave(frm_ctx* ctx) {
+  if (ctx->last_is_ring) return ring_materialize(ctx);
+  return ring_quiesce(ctx);
+}
+
 int group_synchronize(frm_ctx* ctx) {
   for (uint32_t r = 1; r < ctx->group->n; ++r) {
     frm_ctx* c = ctx->group->sub[r];
@@ -739,6 +1082,11 @@ static int create_one(const frm_config* config, int device, frm_ctx** out_ctx) {
   ctx->flags = config->flags;
   ctx->nslots = config->frames_in_flight ? config->frames_in_flight : 1u;
   if (const char* env = getenv("FRM_SCHED")) ctx->fused_sched = strcmp(env, "sort") != 0;
+  if (const char* env = getenv("FRM_RING")) ctx->ring_enabled = strcmp(env, "0") != 0;  // A/B: per-frame grids
+  if (const char* env = getenv("FRM_RING_SERVICE")) {  // service waves of a ring grid (tuning)
+    long v = strtol(env, nullptr, 10);
+    if (v >= 1 && v <= 1024) ctx->ring.service_waves = (uint32_t)v;
+  }
   if (const char* env = getenv("FRM_SERVICE_MIN")) {
     long v = strtol(env, nullptr, 10);
     if (v >= 1 && v <= 64) ctx->service_min = (uint32_t)v;
@@ -891,6 +1239,16 @@ int frm_destroy(frm_ctx* ctx) {
   }
   // Teardown is best effort: statuses are ignored so every resource gets released.
   (void)hipSetDevice(ctx->device);
+  {
+    Ring& R = ctx->ring;
+    if (R.grid_id) (void)ring_quiesce(ctx);
+    ring_free_buffers(R);
+    ring_free_images(R);
+    for (const Ring::Retired& r : R.retired) (void)hipHostFree(r.img);
+    R.retired.clear();
+    if (R.dev) (void)hipFree(R.dev);
+    if (R.host) (void)hipHostFree(R.host);
+  }
   for (uint32_t i = 0; i < ctx->nslots; ++i) {
     Slot& sl = ctx->slots[i];
     if (sl.stream) (void)hipStreamSynchronize(sl.stream);
@@ -944,6 +1302,9 @@ int frm_resize(frm_ctx* ctx, uint32_t width, uint32_t height) {
     return FRM_OK;
   }
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  // ring frames in flight finish first (a ring serves one size); their tickets keep their images
+  if (int rc = ring_quiesce(ctx)) return rc;
+  if (width != ctx->width || height != ctx->height) ctx->last_is_ring = false;
   if (ctx->slots[0].fb && width == ctx->width && height == ctx->height) return FRM_OK;
   if (!ctx->slots[0].stream) return fail(ctx, FRM_ERR_HIP, "context stream missing");
   // No drain: frames in flight finish at their own size. Every buffer that follows the size grows
@@ -984,7 +1345,10 @@ int frm_render(frm_ctx* ctx, frm_stats* stats) {
   int rc = ensure_ready(ctx);
   if (rc) return rc;
   if (ctx->group) return group_render(ctx, stats);
+  if (!stats && ring_eligible(ctx)) return ring_render(ctx);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if ((rc = ring_quiesce(ctx))) return rc;  // a frame outside the ring: the ring's frames first
+  ctx->last_is_ring = false;
   if (stats && (rc = synchronize_all(ctx))) return rc;  // the counters must hold this frame alone
   const uint32_t si = ctx->next_slot;
   Slot& sl = ctx->slots[si];
@@ -1027,6 +1391,7 @@ int frm_read_frame(frm_ctx* ctx, uint8_t* dst, size_t dst_bytes) {
   if (dst_bytes < need)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, frame needs %zu", dst_bytes, need);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (int rc = ring_materialize(ctx)) return rc;
   const Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
   FRM_HIP(ctx, hipMemcpyAsync(dst, sl.fb, need, hipMemcpyDeviceToHost, sl.stream));
   FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
@@ -1044,6 +1409,7 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
   if (dst_bytes < need)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, output needs %zu", dst_bytes, need);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (int rc = ring_materialize(ctx)) return rc;
   const Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
   if (need > ctx->present_cap) {
     FRM_HIP(ctx, hipStreamSynchronize(sl.stream));
@@ -1097,8 +1463,9 @@ static int readback_async(frm_ctx* ctx, Slot& sl, const uint8_t* src, size_t byt
 int frm_read_frame_async(frm_ctx* ctx, uint64_t* out_ticket) {
   if (!ctx || !out_ticket) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/out_ticket is NULL");
   if (!ctx->width) return fail(ctx, FRM_ERR_NOT_READY, "frm_resize has not been called");
-  if (!ctx->render_seq) return fail(ctx, FRM_ERR_NOT_READY, "no frm_render since the context was created");
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->last_is_ring) return ring_read_async(ctx, out_ticket);
+  if (!ctx->render_seq) return fail(ctx, FRM_ERR_NOT_READY, "no frm_render since the context was created");
   Slot& sl = ctx->slots[ctx->last_slot];  // the frame of the last frm_render
   int rc = copy_stream_after_render(ctx, sl);
   if (rc) return rc;
@@ -1113,6 +1480,7 @@ int frm_present_async(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uin
     return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "bad output size %ux%u", out_width, out_height);
   if (flags & ~(FRM_BLIT_SRGB | FRM_BLIT_BGRA)) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (int rc = ring_materialize(ctx)) return rc;
   Slot& sl = ctx->slots[ctx->last_slot];
   const size_t need = (size_t)out_width * out_height * 4u;
   int rc = copy_stream_after_render(ctx, sl);
@@ -1131,6 +1499,24 @@ int frm_present_async(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uin
 
 int frm_frame_pixels(frm_ctx* ctx, uint64_t ticket, const uint8_t** out_pixels, size_t* out_bytes) {
   if (!ctx || !out_pixels) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "ctx/out_pixels is NULL");
+  if (ticket) {  // a ring frame's zero-copy image: wait for the frame (its shading wrote the image)
+    Ring& R = ctx->ring;
+    for (uint32_t s = 0; s < kRingSlots; ++s)
+      for (uint32_t par = 0; par < 2; ++par)
+        if (R.img_ticket[s][par] == ticket) {
+          if (int rc = ring_wait(ctx, s, R.img_seq[s][par])) return rc;
+          *out_pixels = reinterpret_cast<const uint8_t*>(R.img[s][par]);
+          if (out_bytes) *out_bytes = R.img_bytes[s][par];
+          return FRM_OK;
+        }
+    for (const Ring::Retired& r : R.retired)
+      if (r.ticket == ticket) {
+        if (int rc = ring_wait(ctx, r.slot, r.seq)) return rc;
+        *out_pixels = reinterpret_cast<const uint8_t*>(r.img);
+        if (out_bytes) *out_bytes = r.bytes;
+        return FRM_OK;
+      }
+  }
   for (uint32_t i = 0; i < ctx->nslots && ticket; ++i) {
     Slot& sl = ctx->slots[i];
     if (sl.copy_ticket != ticket) continue;
@@ -1159,6 +1545,10 @@ int frm_reload(frm_ctx* ctx, const char* source_dir) {
         return fail(ctx, rc, "reload failed, previous kernels kept: %s", log.c_str());
       }
     }
+  if (int rc = ring_leave(ctx)) {
+    for (uint32_t r = 0; r < n; ++r) unload_reloaded(rk[r]);
+    return rc;
+  }
   for (uint32_t r = 0; r < n; ++r) {
     frm_ctx* c = member(ctx, r);
     // the old module may still run, on this context's stream or a caller's (frm_render_bands)
@@ -1175,6 +1565,7 @@ int frm_synchronize(frm_ctx* ctx) {
   if (!ctx) return fail(nullptr, FRM_ERR_INVALID_ARGUMENT, "ctx is NULL");
   if (ctx->group) return group_synchronize(ctx);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (int rc = ring_quiesce(ctx)) return rc;
   return synchronize_all(ctx);
 }
 
@@ -1211,6 +1602,7 @@ int frm_render_bands(frm_ctx* ctx, uint8_t* dev_dst, size_t dst_bytes, uint32_t 
   if (dst_bytes < need)
     return fail(ctx, FRM_ERR_BUFFER_TOO_SMALL, "dst holds %zu bytes, bands need %zu", dst_bytes, need);
   FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if ((rc = ring_leave(ctx))) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   unsigned long long* counters = dev_counters ? (unsigned long long*)dev_counters : ctx->counters;
   KernelArgs a = make_args(ctx, dev_dst, counters, band_rows, first_band, band_stride, rows);
@@ -1268,6 +1660,8 @@ int frm_render_bands_batch(frm_ctx* ctx, uint32_t count, const frm_parameters* p
                   "(scene, iterations, time-derived constants, aspect)",
                   k);
   }
+  FRM_HIP(ctx, hipSetDevice(ctx->device));
+  if (int rc = ring_leave(ctx)) return rc;
   ctx->params = params[count - 1];  // the context's parameters: the batch's last frame
   compute_scene_uniforms(params[count - 1], ctx->flags, &ctx->scene);
   ctx->has_params = true;
@@ -1334,6 +1728,7 @@ extern "C" int frm_debug_read(frm_ctx* ctx, uint64_t* out5) {
 int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
   if (!ctx || !out) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
   if (ctx->group) return not_on_group(ctx, "frm_debug_pixel_keys");
+  if (int rc = ring_leave(ctx)) return rc;
   const Slot& sl = ctx->slots[(ctx->next_slot + ctx->nslots - 1u) % ctx->nslots];  // last launch
   if (!sl.sched_keys) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "no persistent launch yet");
   if (n > sl.sched_cap) n = sl.sched_cap;
@@ -1348,6 +1743,7 @@ int frm_debug_pixel_keys(frm_ctx* ctx, uint8_t* out, size_t n) {
 int frm_debug_set_pixel_keys(frm_ctx* ctx, const uint8_t* keys, size_t n) {
   if (!ctx || !keys) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "NULL argument");
   if (ctx->group) return not_on_group(ctx, "frm_debug_set_pixel_keys");
+  if (int rc = ring_leave(ctx)) return rc;
   Slot& sl = ctx->slots[ctx->next_slot];
   if (!sl.sched_history || !sl.sched_whole || sl.sched_w != ctx->width || sl.sched_h != ctx->height ||
       n != (size_t)ctx->width * ctx->height || n > sl.sched_cap)
@@ -1367,6 +1763,7 @@ int frm_debug_trace(frm_ctx* ctx, float* out, size_t n_floats) {
   int rc = ensure_ready(ctx);
   if (rc) return rc;
   if (ctx->group) return not_on_group(ctx, "frm_debug_trace");
+  if ((rc = ring_leave(ctx))) return rc;
   if (!out) return fail(ctx, FRM_ERR_INVALID_ARGUMENT, "out is NULL");
   const size_t npix = (size_t)ctx->width * ctx->height;
   if (n_floats < npix * 10u)

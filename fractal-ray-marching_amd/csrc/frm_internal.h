@@ -36,6 +36,120 @@ constexpr uint32_t kRecHit = 1u << 22, kRecSunMiss = 1u << 23;
 constexpr uint32_t kRecKeyShift = 24;
 constexpr size_t kRecordBytes = sizeof(ShadeTail) + sizeof(ShadeGeom);  // scratch per local pixel
 
+// One wave per workgroup: a persistent wave frees its CU slot the moment its last pixel ends, not
+// when the slowest of a 4-wave workgroup's does, so the next frame in flight fills the slots of a
+// draining frame sooner (round 4, profiles/round4/ab_wg: moving-camera drop-in loop 12.62 -> 12.33
+// ms/frame, HEADLINE_FLY 11.96 -> 11.75; headline, C2, C3 and the 8-way share unchanged)
+#ifndef FRM_MARCH_BLOCK
+#define FRM_MARCH_BLOCK 64
+#endif
+constexpr uint32_t kMarchBlock = FRM_MARCH_BLOCK;  // march_persistent threads per workgroup
+// The persistent kernel's work queue (its chunks of 64 fetch positions, most expensive first),
+// XCD-aware. One claim counter for the whole GPU serialised every claim at one address: C3 waves
+// parked 57 % of their cycles in the claim's wait (PMC SQ_WAIT_ANY; tools/diag_waves.py: the refill
+// block took 62 % of wave time). Now the head of the order (its first 1/kQueueHeadDiv chunks, the
+// most expensive) is claimed from one shared counter, so waves of every XCD start the frame's
+// longest pixels first; the rest is dealt round-robin over kQueueParts partitions (chunk c to
+// partition c % kQueueParts, keeping the order's slope in each), one per XCD, each claimed through
+// its own counter in its own 256-B line by the waves of that XCD (HW_REG_XCC_ID); a wave whose
+// partition is drained moves on to the next. C3 1.75 -> 1.11 ms, headline 10.40 -> 10.25 ms, the
+// moving-camera loops within noise (profiles/round4/ab_xq; 32 partitions or a head of 1/32: no
+// better, profiles/round4/ab_qs). Placement only ever changes which lane computes a pixel, never
+// its bytes.
+#ifndef FRM_QUEUE_PARTS
+#define FRM_QUEUE_PARTS 8
+#endif
+#ifndef FRM_QUEUE_HEAD_DIV
+#define FRM_QUEUE_HEAD_DIV 8
+#endif
+constexpr uint32_t kXcds = 8;                           // MI355X
+constexpr uint32_t kQueueParts = FRM_QUEUE_PARTS;       // a multiple of kXcds: kQueueParts / 8 per XCD
+constexpr uint32_t kQueueHeadDiv = FRM_QUEUE_HEAD_DIV;  // the shared head: nchunks / kQueueHeadDiv chunks
+static_assert(kQueueParts % kXcds == 0 && kQueueParts <= 32, "queue partitions: a multiple of the XCDs, <= 32");
+constexpr uint32_t kQueuePartWords = 64;    // u32 words between two counters (256 B); the head's is
+                                            // counter kQueueParts
+constexpr uint32_t kQueueDebugWord = (kQueueParts + 1u) * kQueuePartWords;  // FRM_STAMPS words after the counters
+constexpr size_t kQueueBytes = (kQueueDebugWord + 64u) * 4u;
+constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
+constexpr uint32_t kRankWords = 512;  // one launch's key_hist: 256 counts + 256 cursors
+constexpr uint32_t kShadeBlockPixels = 4096;  // shade_pass / rank_pass: local pixels per 256-thread block
+
+// ---- resident frame ring (frm_api.hip resident_render; march_persistent<..., RES>) ----------
+// Single-frame frm_render calls on a context with frames in flight post their frames to a ring
+// of kRingSlots-or-fewer slots instead of launching a grid per frame. One persistent grid serves
+// the ring for as long as frames keep arriving: its march waves claim the oldest posted frame's
+// chunks and move on to the next frame when that one's queue drains (as a multi-frame launch
+// interleaves its frames), and a few service waves of the same grid shade, rank and publish each
+// frame once its last pixel has marched. Frames are numbered 1, 2, ... (seq); frame g uses slot
+// (g - 1) % slots. The host posts frame g only after frame g - slots is done (its slot is free).
+constexpr uint32_t kRingSlots = 4;
+constexpr uint32_t kRingGridIds = 8;  // RingHost::grid_stop entries (grid id % 8)
+constexpr uint32_t kRingRankPixels = 1024;  // local pixels per rank task (16 per lane)
+
+// One posted frame (pinned host memory; the host writes it before it posts the frame, the
+// device reads it with system-scope loads).
+struct RingFrame {
+  float row[3][4];     // camera_matrix rows (FrameCamera)
+  float ox, oy, oz;    // camera origin
+  float mb_power;      // the Mandelbulb's power at the frame's time (fragment.wgsl:75)
+  uint32_t seq;
+  uint32_t pad0;
+  uint32_t* host_img;  // zero-copy readback: the shading also stores the frame here (or nullptr)
+  uint32_t pad[12];
+};
+static_assert(sizeof(RingFrame) == 128, "RingFrame: 128 bytes");
+
+// Host <-> device words (pinned, fine-grained host memory), each in its own 128-byte line.
+struct RingHost {
+  uint32_t posted;               // host: the last posted seq (release store after the frame's data)
+  uint32_t pad0[31];
+  uint32_t closed;               // device: id of the last grid that closed (stopped taking frames)
+  uint32_t pad1[31];
+  uint32_t grid_stop[kRingGridIds][32];  // host: grid id i serves no frame >= grid_stop[i % 8][0]
+  uint32_t done[kRingSlots][32];         // device: seq of the slot's last completed frame
+  RingFrame frames[kRingSlots];
+};
+
+// Per-slot device state. The claim and completion counters are 64-bit words whose high half is
+// the seq of the frame they count (an "epoch"): the frame that completes a slot writes the next
+// frame's epoch (seq + slots) with a zero count, so a late or stale atomic of an earlier frame
+// sees a foreign epoch and does nothing. Each word sits in its own 256-byte line.
+struct RingSlotCtl {
+  unsigned long long queue[(kQueueParts + 1u) * (kQueuePartWords / 2u)];  // claim counters: partition x at
+                                                                          // x * 32, the head at kQueueParts * 32
+  unsigned long long pix_done[32];    // local pixels whose march has ended
+  unsigned long long shade_next[32];  // shade tasks claimed
+  unsigned long long shade_done[32];  // shade tasks done
+  unsigned long long rank_next[32];   // rank tasks claimed
+  unsigned long long rank_done[32];   // rank tasks done
+  uint32_t hist[kRankWords];          // cost-key histogram (256) + rank cursors (256)
+  uint32_t done_seq[64];              // the slot's last completed frame (device copy of RingHost::done)
+};
+
+struct RingGridCtl {  // per grid launch (zeroed before it)
+  uint32_t closed, limit, limit_valid, pad[61];
+};
+
+struct RingDev {  // device memory, per context
+  uint32_t base;  // the first seq the next grid serves (its predecessor's last + 1)
+  uint32_t pad[63];
+  RingGridCtl grid;
+  RingSlotCtl slot[kRingSlots];
+};
+
+// A grid's view of the ring (KernelArgs::ring).
+struct RingArgs {
+  RingHost* host;
+  RingDev* dev;
+  uint32_t slots;          // ring size R: 2 or 4 (slot = (seq - 1) & (R - 1))
+  uint32_t grid_id;
+  uint32_t first_seq;      // the frame this grid was launched for
+  uint32_t service_waves;  // workgroups 0..service_waves-1 shade, rank and publish
+  uint32_t* out;           // device framebuffers: slot s at out + s * rec_stride words
+  uint32_t* order;         // fetch orders: slot s at order + s * rec_stride
+  uint8_t* keys;           // cost keys: slot s at keys + s * rec_stride
+};
+
 struct KernelArgs {
   FrameUniforms f;
   SceneUniforms s;
@@ -76,45 +190,9 @@ struct KernelArgs {
   // which carries a per-lane power; s.mb_power otherwise.
   float mb_powers[kMaxBatch];
   uint32_t anim;
+  RingArgs ring;  // march_persistent<..., RES = true>: the resident frame ring
 };
-constexpr uint32_t kRankWords = 512;  // one launch's key_hist: 256 counts + 256 cursors
-constexpr uint32_t kShadeBlockPixels = 4096;  // shade_pass / rank_pass: local pixels per 256-thread block
 
-// One wave per workgroup: a persistent wave frees its CU slot the moment its last pixel ends, not
-// when the slowest of a 4-wave workgroup's does, so the next frame in flight fills the slots of a
-// draining frame sooner (round 4, profiles/round4/ab_wg: moving-camera drop-in loop 12.62 -> 12.33
-// ms/frame, HEADLINE_FLY 11.96 -> 11.75; headline, C2, C3 and the 8-way share unchanged)
-#ifndef FRM_MARCH_BLOCK
-#define FRM_MARCH_BLOCK 64
-#endif
-constexpr uint32_t kMarchBlock = FRM_MARCH_BLOCK;  // march_persistent threads per workgroup
-// The persistent kernel's work queue (its chunks of 64 fetch positions, most expensive first),
-// XCD-aware. One claim counter for the whole GPU serialised every claim at one address: C3 waves
-// parked 57 % of their cycles in the claim's wait (PMC SQ_WAIT_ANY; tools/diag_waves.py: the refill
-// block took 62 % of wave time). Now the head of the order (its first 1/kQueueHeadDiv chunks, the
-// most expensive) is claimed from one shared counter, so waves of every XCD start the frame's
-// longest pixels first; the rest is dealt round-robin over kQueueParts partitions (chunk c to
-// partition c % kQueueParts, keeping the order's slope in each), one per XCD, each claimed through
-// its own counter in its own 256-B line by the waves of that XCD (HW_REG_XCC_ID); a wave whose
-// partition is drained moves on to the next. C3 1.75 -> 1.11 ms, headline 10.40 -> 10.25 ms, the
-// moving-camera loops within noise (profiles/round4/ab_xq; 32 partitions or a head of 1/32: no
-// better, profiles/round4/ab_qs). Placement only ever changes which lane computes a pixel, never
-// its bytes.
-#ifndef FRM_QUEUE_PARTS
-#define FRM_QUEUE_PARTS 8
-#endif
-#ifndef FRM_QUEUE_HEAD_DIV
-#define FRM_QUEUE_HEAD_DIV 8
-#endif
-constexpr uint32_t kXcds = 8;                           // MI355X
-constexpr uint32_t kQueueParts = FRM_QUEUE_PARTS;       // a multiple of kXcds: kQueueParts / 8 per XCD
-constexpr uint32_t kQueueHeadDiv = FRM_QUEUE_HEAD_DIV;  // the shared head: nchunks / kQueueHeadDiv chunks
-static_assert(kQueueParts % kXcds == 0 && kQueueParts <= 32, "queue partitions: a multiple of the XCDs, <= 32");
-constexpr uint32_t kQueuePartWords = 64;    // u32 words between two counters (256 B); the head's is
-                                            // counter kQueueParts
-constexpr uint32_t kQueueDebugWord = (kQueueParts + 1u) * kQueuePartWords;  // FRM_STAMPS words after the counters
-constexpr size_t kQueueBytes = (kQueueDebugWord + 64u) * 4u;
-constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
 
 #if !defined(__HIPCC_RTC__)  // host-side launchers; hiprtc only needs the types above
 // Render kernels compiled at run time from edited sources (frm_reload.hip), per DE family
@@ -136,6 +214,8 @@ enum KernelKind : uint32_t { kKernelPersistent = 0, kKernelSimple = 1 };
 // blocks_cap: at most this many persistent workgroups (one wave each) per CU; 0 = the occupancy limit
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
                          const ReloadedKernels* rk, int blocks_cap = 0);
+// A resident ring grid (RingArgs in args.ring) on `stream`; *out_blocks: its workgroups.
+hipError_t launch_ring(const KernelArgs& args, int cu_count, hipStream_t stream, int* out_blocks);
 hipError_t launch_blit(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh,
                        uint32_t flags, hipStream_t stream);
 hipError_t launch_unshuffle(const uint8_t* src, size_t rank_stride, uint8_t* dst, uint32_t width,

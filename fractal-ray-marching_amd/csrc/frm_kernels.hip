@@ -227,6 +227,46 @@ static hipError_t launch_family(const KernelArgs& args, KernelKind kind, int cu_
   return hipGetLastError();
 }
 
+// A resident ring grid (frm_api.hip resident_render): the occupancy limit of the RES instantiation
+// (the Mandelbulb's with per-lane powers: ring frames differ in time) over every CU, the first
+// args.ring.service_waves workgroups serving the ring (frm_render_kernels.h ring_service).
+template <uint32_t FAM, bool ITERS>
+static hipError_t launch_ring_fam(const KernelArgs& args, int cu_count, hipStream_t stream, int* out_blocks) {
+  constexpr bool kAnim = is_mandelbulb(FAM);
+  static int blocks_per_cu = 0;
+  if (blocks_per_cu == 0) {
+    int n = 0;
+    hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, march_persistent<FAM, ITERS, false, kAnim, true>, kMarchBlock, 0);
+    if (e != hipSuccess) return e;
+    blocks_per_cu = n > 0 ? n : 1;
+  }
+  int bpc = blocks_per_cu;
+  if (const int v = blocks_override()) bpc = v;
+  const uint32_t blocks = (uint32_t)(bpc * cu_count);
+  if (out_blocks) *out_blocks = (int)blocks;
+  if (args.ring.service_waves >= blocks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((march_persistent<FAM, ITERS, false, kAnim, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+  return hipGetLastError();
+}
+
+template <uint32_t FAM>
+static hipError_t launch_ring_family(const KernelArgs& args, int cu_count, hipStream_t stream, int* out_blocks) {
+  return args.s.n ? launch_ring_fam<FAM, true>(args, cu_count, stream, out_blocks)
+                  : launch_ring_fam<FAM, false>(args, cu_count, stream, out_blocks);
+}
+
+hipError_t launch_ring(const KernelArgs& args, int cu_count, hipStream_t stream, int* out_blocks) {
+  switch (args.s.family) {
+    case kMenger: return launch_ring_family<kMenger>(args, cu_count, stream, out_blocks);
+    case kSierpinski: return launch_ring_family<kSierpinski>(args, cu_count, stream, out_blocks);
+    case kKoch: return launch_ring_family<kKoch>(args, cu_count, stream, out_blocks);
+    case kMandelbulb: return launch_ring_family<kMandelbulb>(args, cu_count, stream, out_blocks);
+    case kMandelbulbHw: return launch_ring_family<kMandelbulbHw>(args, cu_count, stream, out_blocks);
+    default: return launch_ring_family<kSphere>(args, cu_count, stream, out_blocks);
+  }
+}
+
 hipError_t launch_render(const KernelArgs& args, KernelKind kind, int cu_count, hipStream_t stream,
                          const ReloadedKernels* rk, int blocks_cap) {
   switch (args.s.family) {

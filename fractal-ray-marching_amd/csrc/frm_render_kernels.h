@@ -95,6 +95,466 @@ __device__ __forceinline__ uint8_t cost_key(uint32_t bodies) {
   return (uint8_t)min(255.0f, 16.0f * __log2f((float)bodies + 1.0f));
 }
 
+// ---- resident frame ring: device side (frm_internal.h RingArgs) ----------------------------
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t dev_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long dev_load64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void dev_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+constexpr uint64_t kRingWatchdogTicks = 200000000ull;  // 2 s of the 100 MHz clock without progress
+constexpr unsigned long long kEpochMask = 0xFFFFFFFF00000000ull;
+__device__ __forceinline__ unsigned long long epoch_of(uint32_t seq) { return (unsigned long long)seq << 32; }
+
+// Lane 0's 64-bit atomic add of `v` to an epoch-tagged counter (one lane: a vector atomic),
+// broadcast: the count before the add when the word still counts frame `seq`, else ~0u.
+__device__ __forceinline__ uint32_t epoch_add(unsigned long long* w, uint32_t seq, uint32_t v) {
+  unsigned long long old = 0;
+  if ((threadIdx.x & 63u) == 0) {
+    // a word that already counts another frame is left alone (frm_internal.h RingSlotCtl)
+    const unsigned long long cur = dev_load64(w);
+    old = (cur & kEpochMask) == epoch_of(seq) ? atomicAdd(w, (unsigned long long)v) : cur;
+  }
+  old = __shfl(old, 0, 64);
+  return (old & kEpochMask) == epoch_of(seq) ? (uint32_t)old : 0xFFFFFFFFu;
+}
+
+// epoch_add for a claim counter of `n` items: no atomic once the word counts n or more (or another
+// frame), so claims that find the counter exhausted leave it alone; ~0u when nothing was claimed.
+__device__ __forceinline__ uint32_t epoch_add_below(unsigned long long* w, uint32_t seq, uint32_t n) {
+  unsigned long long old = 0;
+  if ((threadIdx.x & 63u) == 0) {
+    const unsigned long long cur = dev_load64(w);
+    old = ((cur & kEpochMask) == epoch_of(seq) && (uint32_t)cur < n) ? atomicAdd(w, 1ull) : ~0ull;
+  }
+  old = __shfl(old, 0, 64);
+  return (old & kEpochMask) == epoch_of(seq) && (uint32_t)old < n ? (uint32_t)old : 0xFFFFFFFFu;
+}
+// A task claim that never moves a counter past n: compare-and-swap from a count below n. Once every
+// task of a frame is claimed no claim touches the word again, so the frame's completion (which
+// resets the word for the slot's next frame) cannot race with a late claim.
+__device__ __forceinline__ uint32_t epoch_claim(unsigned long long* w, uint32_t seq, uint32_t n) {
+  uint32_t got = 0xFFFFFFFFu;
+  if ((threadIdx.x & 63u) == 0) {
+    unsigned long long cur = dev_load64(w);
+    while ((cur & kEpochMask) == epoch_of(seq) && (uint32_t)cur < n) {
+      const unsigned long long prev = atomicCAS(w, cur, cur + 1ull);
+      if (prev == cur) {
+        got = (uint32_t)cur;
+        break;
+      }
+      cur = prev;
+    }
+  }
+  return uniform(__shfl(got, 0, 64));
+}
+
+// The frames a grid may serve: those up to min(posted, grid_stop - 1), and after the grid has
+// closed (a march wave found nothing left to claim), those up to the limit its closer fixed.
+struct RingView {
+  uint32_t limit;  // the last seq this wave knows it may serve
+  bool closed;     // `limit` is the grid's final limit
+};
+__device__ __forceinline__ void ring_refresh(const RingArgs& r, RingView& v) {
+  if (v.closed) return;
+  uint32_t lim = 0, closed = 0;
+  if ((threadIdx.x & 63u) == 0) {
+    closed = dev_load(&r.dev->grid.limit_valid);
+    if (closed) {
+      lim = dev_load(&r.dev->grid.limit);
+    } else {
+      const uint32_t posted = sys_load(&r.host->posted);
+      const uint32_t stop = sys_load(&r.host->grid_stop[r.grid_id % kRingGridIds][0]);
+      lim = min(posted, stop - 1u);
+    }
+  }
+  v.closed = uniform(__shfl(closed, 0, 64)) != 0;
+  v.limit = uniform(__shfl(lim, 0, 64));
+}
+// A march wave with nothing left to claim up to v.limit closes the grid: the first to get there
+// publishes (to the host, then after a system-scope fence reads `posted` once more) the last frame
+// the grid serves; every other wave waits for that limit. Frames posted later belong to the next
+// grid, which the host launches when it sees `closed` (frm_api.hip resident_render).
+__device__ __forceinline__ void ring_close(const RingArgs& r, RingView& v) {
+  uint32_t lim = 0, ok = 1;
+  if ((threadIdx.x & 63u) == 0) {
+    if (atomicCAS(&r.dev->grid.closed, 0u, 1u) == 0u) {
+      sys_store(&r.host->closed, r.grid_id);
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);  // system scope: the store above before the loads below
+      const uint32_t posted = sys_load(&r.host->posted);
+      const uint32_t stop = sys_load(&r.host->grid_stop[r.grid_id % kRingGridIds][0]);
+      lim = min(posted, stop - 1u);
+      dev_store(&r.dev->grid.limit, lim);
+      dev_store(&r.dev->base, lim + 1u);
+      dev_store(&r.dev->grid.limit_valid, 1u);
+    } else {
+      const uint64_t t0 = realtime();
+      while (!dev_load(&r.dev->grid.limit_valid)) {
+        if (realtime() - t0 > 1000000ull) { ok = 0; break; }  // 10 ms: the closer stalled; stop here
+        __builtin_amdgcn_s_sleep(2);
+      }
+      lim = dev_load(&r.dev->grid.limit);
+    }
+  }
+  v.closed = true;
+  v.limit = uniform(__shfl(ok ? lim : 0u, 0, 64));
+}
+
+// The camera of ring frame `seq` into wave-uniform registers (system-scope loads of its RingFrame).
+struct RingCam {
+  float row[3][4];
+  v3 origin;
+  float power;
+  uint32_t* host_img;
+};
+// The first 16 words of ring frame `slot`'s RingFrame (camera rows, origin, power) into LDS.
+__device__ __forceinline__ void ring_camera_lds(const RingArgs& r, uint32_t slot, float* lds) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&r.host->frames[slot]);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (lane < 16u) lds[lane] = __uint_as_float(sys_load(w + lane));
+  __syncthreads();  // one-wave workgroup: orders the LDS accesses
+}
+__device__ __forceinline__ RingCam ring_camera(const RingArgs& r, uint32_t slot) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&r.host->frames[slot]);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t mine = lane < 20u ? sys_load(w + lane) : 0u;  // row[12], origin[3], power, seq, pad, host_img
+  RingCam c;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) c.row[i / 4][i % 4] = __uint_as_float(uniform(__shfl(mine, i, 64)));
+  c.origin = mk(__uint_as_float(uniform(__shfl(mine, 12, 64))), __uint_as_float(uniform(__shfl(mine, 13, 64))),
+                __uint_as_float(uniform(__shfl(mine, 14, 64))));
+  c.power = __uint_as_float(uniform(__shfl(mine, 15, 64)));
+  const uint64_t lo = uniform(__shfl(mine, 18, 64)), hi = uniform(__shfl(mine, 19, 64));
+  c.host_img = reinterpret_cast<uint32_t*>(lo | (hi << 32));
+  return c;
+}
+
+// A ring march wave's claim state, in LDS (its SGPRs are the march's): the frame it claims from,
+// the frame of its last claimed chunk (slot), the grid's frames as it last saw them, and per slot the
+// pixels whose march ended in this wave and that the slot's pix_done does not count yet. Those are
+// added when the wave claims a chunk of that frame (it then still holds unfinished pixels of it) or
+// once it has moved past the frame (it never claims from it again), so a frame's count completes
+// only after every wave is done claiming from it.
+enum RingWaveWord : uint32_t { kRwSeq = 0, kRwCamSeq, kRwSlot, kRwLimit, kRwClosed, kRwPend, kRwWords = kRwPend + kRingSlots };
+__device__ __forceinline__ uint32_t rw_get(const uint32_t* rw, uint32_t i) { return uniform(rw[i]); }
+__device__ __forceinline__ void rw_set(uint32_t* rw, uint32_t i, uint32_t v) {
+  if ((threadIdx.x & 63u) == 0) rw[i] = v;
+}
+// Records of a ring frame are read by the service waves' shading, which may run on another XCD:
+// the L2s of the XCDs are not coherent with each other, so the march writes them through to memory
+// (agent-scope stores, `sc1`) and waits for them (ring_flush) before it counts their pixels; the
+// shading's acquire of the count then invalidates its own L2 before it reads them.
+__device__ __forceinline__ void coherent_store(ShadeTail* p, uint2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void coherent_store(ShadeGeom* p, float4 v) {
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(w, (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 1, (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Adds slot sl's pending count to its frame's pix_done, after the wave's record stores have
+// completed (coherent_store: written through, so completion is visibility at agent scope).
+__device__ __forceinline__ void ring_flush(const KernelArgs& a, uint32_t* rw, uint32_t sl) {
+  const uint32_t pv = rw_get(rw, kRwPend + sl);
+  if (!pv) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t seq = rw_get(rw, kRwCamSeq) - ((rw_get(rw, kRwSlot) - sl) & (a.ring.slots - 1u));
+  (void)epoch_add(&a.ring.dev->slot[sl].pix_done[0], seq, pv);
+  rw_set(rw, kRwPend + sl, 0u);
+}
+// The pixels of finished-lane mask fm (record index pix = slot * rec_stride + local pixel) into the
+// per-slot pending counts; frames the wave has moved past are flushed at once.
+__device__ __forceinline__ void ring_count_fins(const KernelArgs& a, uint32_t* rw, uint64_t fm, uint32_t pix) {
+  const uint32_t R = a.ring.slots, rs = a.rec_stride;
+  uint32_t prev = 0;
+#pragma unroll
+  for (uint32_t sl = 0; sl < kRingSlots; ++sl) {
+    if (sl >= R) break;
+    const uint32_t cum = sl + 1u < R ? (uint32_t)__popcll(fm & ballot(pix < (sl + 1u) * rs))
+                                     : (uint32_t)__popcll(fm);
+    if (cum != prev) rw_set(rw, kRwPend + sl, rw_get(rw, kRwPend + sl) + (cum - prev));
+    prev = cum;
+  }
+  const uint32_t rslot = rw_get(rw, kRwSlot);
+  const bool moved = rw_get(rw, kRwSeq) != rw_get(rw, kRwCamSeq);
+#pragma unroll
+  for (uint32_t sl = 0; sl < kRingSlots; ++sl)
+    if (sl < R && (sl != rslot || moved)) ring_flush(a, rw, sl);
+}
+// The next chunk for a ring march wave: the oldest of the grid's frames with chunks left. Returns
+// the chunk's first fetch position (kIdle: nothing left for this grid); the frame's slot in
+// rw[kRwSlot] and its camera in cam_lds. `drained`/`part` as in the single-frame claim.
+__device__ __forceinline__ uint32_t ring_claim(const KernelArgs& a, uint32_t* rw, float* cam_lds, uint64_t& drained,
+                                               uint32_t& part, uint32_t nchunks, uint32_t nhead) {
+  const uint32_t R = a.ring.slots;
+  for (;;) {
+    uint32_t seq = rw_get(rw, kRwSeq);
+    if (seq > rw_get(rw, kRwLimit)) {
+      RingView v = {rw_get(rw, kRwLimit), rw_get(rw, kRwClosed) != 0};
+      ring_refresh(a.ring, v);
+      if (seq > v.limit && !v.closed) ring_close(a.ring, v);
+      rw_set(rw, kRwLimit, v.limit);
+      rw_set(rw, kRwClosed, v.closed ? 1u : 0u);
+      if (seq > v.limit) return kIdle;  // nothing left for this grid
+    }
+    if (seq != rw_get(rw, kRwCamSeq)) {  // a frame this wave has not claimed from yet
+      const uint32_t slot = (seq - 1u) & (R - 1u);
+      ring_camera_lds(a.ring, slot, cam_lds);
+      rw_set(rw, kRwSlot, slot);
+      rw_set(rw, kRwCamSeq, seq);
+      drained = 0;
+      part = queue_part();
+    }
+    const uint32_t slot = rw_get(rw, kRwSlot);
+    unsigned long long* q = a.ring.dev->slot[slot].queue;
+    constexpr uint32_t kW = kQueuePartWords / 2u;
+    uint32_t base = kIdle;
+    if (!(drained >> kQueueParts)) {
+      const uint32_t j = epoch_add_below(q + kQueueParts * kW, seq, nhead);
+      if (j < nhead)
+        base = j * kChunk;
+      else
+        drained |= 1ull << kQueueParts;
+    }
+    while (base == kIdle) {
+      // partition `part` holds chunks nhead + j * kQueueParts + part below nchunks
+      const uint32_t jmax = nchunks > nhead + part ? (nchunks - nhead - part + kQueueParts - 1u) / kQueueParts : 0u;
+      const uint32_t j = epoch_add_below(q + part * kW, seq, jmax);
+      const uint32_t c = j == kIdle ? nchunks : nhead + j * kQueueParts + part;
+      if (c < nchunks) {
+        base = c * kChunk;
+        break;
+      }
+      drained |= 1ull << part;
+      if ((drained & ((1ull << kQueueParts) - 1ull)) == (1ull << kQueueParts) - 1ull) break;
+      do part = (part + 1u) % kQueueParts;
+      while ((drained >> part) & 1u);
+    }
+    if (base != kIdle) {
+      ring_flush(a, rw, slot);  // the wave holds unfinished pixels of this frame: its count stays short
+      return base;
+    }
+    rw_set(rw, kRwSeq, seq + 1u);  // drained for this wave: it never claims from that frame again
+    ring_flush(a, rw, slot);
+  }
+}
+
+// Wave-wide exclusive prefix sum of one value per lane.
+__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(inc, off, 64);
+    if (lane >= (uint32_t)off) inc += u;
+  }
+  return inc - v;
+}
+
+// Shade task t of ring frame `seq` (slot s): kShadeBlockPixels local pixels, 64 at a time, as
+// shade_pass (fragment.wgsl:333-348 + the Rgba8UnormSrgb store) with the frame's ring camera; the
+// cost keys go out for the slot's next fetch order and into the frame's key histogram.
+template <uint32_t FAM>
+__device__ void ring_shade_task(const KernelArgs& a, const RingCam& cam, uint32_t s, uint32_t t,
+                                const float* table, uint32_t* cnt) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t width = a.f.width, npix = a.npix, rs = a.rec_stride;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) cnt[lane * 4u + k] = 0u;
+  __syncthreads();  // one-wave workgroup: orders the LDS accesses
+  for (uint32_t j = 0; j < kShadeBlockPixels / 64u; ++j) {
+    const uint32_t idx = t * kShadeBlockPixels + j * 64u + lane;
+    if (idx >= npix) break;
+    const uint32_t lr = idx / width, x = idx - lr * width;
+    const uint32_t y = band_row_to_global(a.g, lr);
+    const uint32_t rec = s * rs + idx;
+    const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[rec]);
+    const uint32_t key = r1.y >> kRecKeyShift;
+    a.ring.keys[rec] = (uint8_t)key;
+    atomicAdd(&cnt[key], 1u);
+    uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
+    if (r1.y & kRecHit) {
+      const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[rec]);
+      const v3 dir = camera_ray_rows(a.f, cam.row, x, y);
+      const v3 hp = ray_at(cam.origin, r0.x, dir);
+      const v3 n = mk(r0.y, r0.z, r0.w);
+      float spec;
+      v3 color = shade_hit_pre(a.f, scene_color<FAM>(hp), dir, n, r1.y & kRecStepsMask, &spec);
+      color = shade_hit_post(color, spec, (r1.y & kRecSunMiss) ? -kInfinity : 0.0f, __uint_as_float(r1.x));
+      word = pack_rgba(color, table);
+    }
+    a.ring.out[rec] = word;
+    if (cam.host_img) cam.host_img[idx] = word;  // zero-copy readback (pinned host image)
+  }
+  __syncthreads();
+  uint32_t* hist = a.ring.dev->slot[s].hist;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (const uint32_t c = cnt[lane * 4u + k]) atomicAdd(&hist[lane * 4u + k], c);
+}
+
+// Rank task t of ring frame `seq` (slot s): kRingRankPixels local pixels into the slot's next fetch
+// order, by descending cost key (rank_pass's counting sort: bucket bases from the frame's complete
+// histogram, a range per task and key reserved through the cursors hist[256..511]; each pixel's
+// place in its range from an LDS atomic). Placement only: never a pixel's bytes.
+__device__ __forceinline__ void ring_rank_task(const KernelArgs& a, uint32_t s, uint32_t t, uint32_t* cnt,
+                                               uint32_t* base) {
+  constexpr uint32_t kPer = kRingRankPixels / 64u;
+  const uint32_t lane = threadIdx.x & 63u, npix = a.npix, rs = a.rec_stride;
+  const uint8_t* keys = a.ring.keys + (size_t)s * rs;
+  uint32_t* order = a.ring.order + (size_t)s * rs;
+  uint32_t* hist = a.ring.dev->slot[s].hist;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) cnt[lane * 4u + k] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    const uint32_t idx = t * kRingRankPixels + j * 64u + lane;
+    if (idx < npix) atomicAdd(&cnt[keys[idx]], 1u);
+  }
+  __syncthreads();
+  // descending key order: lane l holds keys 255 - 4l .. 252 - 4l; base[k] = pixels with a key above
+  // k plus this task's reserved offset in bucket k
+  uint32_t h[4], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    h[i] = hist[255u - (lane * 4u + i)];
+    sum += h[i];
+  }
+  uint32_t before = wave_exclusive_scan(sum);
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t k = 255u - (lane * 4u + i);
+    const uint32_t c = cnt[k];
+    base[k] = before + (c ? atomicAdd(&hist[256u + k], c) : 0u);
+    before += h[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    const uint32_t idx = t * kRingRankPixels + j * 64u + lane;
+    if (idx < npix) {
+      const uint32_t pos = atomicAdd(&base[keys[idx]], 1u);
+      if (pos < npix) order[pos] = idx;  // always, for a histogram of these keys
+    }
+  }
+}
+
+// Every task of ring frame `seq` (slot s) is done: reset the slot for frame seq + slots (the next
+// frame's epoch on every counter, histogram and cursors zeroed), then publish the frame.
+__device__ __forceinline__ void ring_finish(const KernelArgs& a, uint32_t seq, uint32_t s) {
+  const uint32_t lane = threadIdx.x & 63u;
+  RingSlotCtl& c = a.ring.dev->slot[s];
+  const unsigned long long next = epoch_of(seq + a.ring.slots);
+  if (lane <= kQueueParts) c.queue[lane * (kQueuePartWords / 2u)] = next;
+  if (lane == 16u) c.pix_done[0] = next;
+  if (lane == 17u) c.shade_next[0] = next;
+  if (lane == 18u) c.shade_done[0] = next;
+  if (lane == 19u) c.rank_next[0] = next;
+  if (lane == 20u) c.rank_done[0] = next;
+#pragma unroll
+  for (uint32_t k = 0; k < kRankWords / 64u; ++k) c.hist[k * 64u + lane] = 0u;
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);  // system scope: the reset and every shaded pixel first
+  if (lane == 0) {
+    dev_store(&c.done_seq[0], seq);
+    sys_store(&a.ring.host->done[s][0], seq);
+  }
+}
+
+// A ring grid's service wave: shades, ranks and publishes the grid's frames as their marches
+// complete (oldest first, any of the `slots` frames in flight), until the grid has closed and
+// every frame up to its limit is done. Sleeps between polls; gives up after kRingWatchdogTicks
+// without progress (the host then reports the frame as never completed, frm_api.hip).
+template <uint32_t FAM>
+__device__ void ring_service(const KernelArgs& a, float* table, uint32_t* cnt, uint32_t* base) {
+  const RingArgs& R = a.ring;
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) table[lane * 4u + k] = kSrgbThresholds[lane * 4u + k];
+  const uint32_t npix = a.npix;
+  const uint32_t nsh = (npix + kShadeBlockPixels - 1u) / kShadeBlockPixels;
+  const uint32_t nrk = (npix + kRingRankPixels - 1u) / kRingRankPixels;
+  uint32_t seq0 = 0;
+  if (lane == 0) seq0 = max(R.first_seq, dev_load(&R.dev->base));
+  seq0 = uniform(__shfl(seq0, 0, 64));
+  RingView rv = {0u, false};
+  uint64_t last_progress = realtime();
+  unsigned long long last_pd = 0;
+  for (;;) {
+    if (seq0 > rv.limit) ring_refresh(R, rv);
+    // skip the frames already done (another service wave finished them)
+    for (;;) {
+      if (seq0 > rv.limit) break;
+      uint32_t d = 0;
+      if (lane == 0) d = dev_load(&R.dev->slot[(seq0 - 1u) & (R.slots - 1u)].done_seq[0]);
+      if (uniform(__shfl(d, 0, 64)) < seq0) break;
+      ++seq0;
+    }
+    if (seq0 > rv.limit) {
+      if (rv.closed) return;  // every frame of this grid is done
+      if (realtime() - last_progress > kRingWatchdogTicks) return;
+      __builtin_amdgcn_s_sleep(32);
+      continue;
+    }
+    bool worked = false;
+    for (uint32_t g = seq0; g <= rv.limit && g < seq0 + R.slots && !worked; ++g) {
+      const uint32_t s = (g - 1u) & (R.slots - 1u);
+      RingSlotCtl& c = R.dev->slot[s];
+      unsigned long long pd = 0, sd = 0;
+      if (lane == 0) {
+        pd = dev_load64(&c.pix_done[0]);
+        sd = dev_load64(&c.shade_done[0]);
+      }
+      pd = __shfl(pd, 0, 64);
+      sd = __shfl(sd, 0, 64);
+      if (g == seq0 && pd != last_pd) {  // the oldest frame's march moves: progress
+        last_pd = pd;
+        last_progress = realtime();
+      }
+      if (pd != (epoch_of(g) | npix)) continue;  // its march has not ended yet
+      if (sd == (epoch_of(g) | nsh)) {
+        const uint32_t t = epoch_claim(&c.rank_next[0], g, nrk);
+        if (t >= nrk) continue;
+        ring_rank_task(a, s, t, cnt, base);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        if (epoch_add(&c.rank_done[0], g, 1u) == nrk - 1u) {
+          __atomic_thread_fence(__ATOMIC_ACQUIRE);
+          ring_finish(a, g, s);
+        }
+        worked = true;
+      } else {
+        const uint32_t t = epoch_claim(&c.shade_next[0], g, nsh);
+        if (t >= nsh) continue;
+        const RingCam cam = ring_camera(R, s);
+        ring_shade_task<FAM>(a, cam, s, t, table, cnt);
+        __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the pixels (host image too) first
+        epoch_add(&c.shade_done[0], g, 1u);
+        worked = true;
+      }
+    }
+    if (worked) {
+      last_progress = realtime();
+    } else {
+      if (realtime() - last_progress > kRingWatchdogTicks) return;
+      __builtin_amdgcn_s_sleep(16);
+    }
+  }
+}
+
 #ifdef FRM_STAMPS
 // diagnostic build: one 16 x u64 record per wave of the last persistent launch
 constexpr uint32_t kWaveDebugSlots = 16384u;
@@ -107,12 +567,26 @@ __device__ unsigned long long g_wave_debug[16u * kWaveDebugSlots];
 // is wave-uniform.
 // ANIM (MULTI, Mandelbulb): the frames of the launch differ in time, so in the power; each lane
 // carries its pixel's frame's power (a.mb_powers) instead of the uniform one.
-template <uint32_t FAM, bool ITERS, bool MULTI = false, bool ANIM = false>
+// RES: a resident ring grid (frm_internal.h RingArgs): workgroups below a.ring.service_waves run
+// ring_service; the others march the ring's frames in posting order, each frame's chunks as a
+// single-frame launch's, moving on to the next frame when one's queue drains. A lane's record index
+// is slot * rec_stride + its local pixel (as a multi-frame launch's frame * rec_stride + ...).
+template <uint32_t FAM, bool ITERS, bool MULTI = false, bool ANIM = false, bool RES = false>
 #ifndef FRM_MARCH_WAVES_PER_SIMD
 #define FRM_MARCH_WAVES_PER_SIMD 1
 #endif
 __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
   __shared__ float4 chunk_rays[kMarchWaves][kChunk];  // per wave: camera ray xyz + record index bits
+  static_assert(!RES || (!MULTI && kMarchWaves == 1u), "ring grids: one-wave workgroups, one frame per chunk");
+  __shared__ float cam_lds[RES ? 16 : 1];  // RES: the camera of the wave's current frame (rows, origin, power)
+  __shared__ uint32_t rw[RES ? (uint32_t)kRwWords : 1u];  // RES: the wave's claim state (RingWaveWord)
+  if constexpr (RES) {
+    __shared__ uint32_t svc_lds[768];  // service waves: sRGB table, key counts, bucket bases
+    if (blockIdx.x < a.ring.service_waves) {
+      ring_service<FAM>(a, reinterpret_cast<float*>(svc_lds), svc_lds + 256, svc_lds + 512);
+      return;
+    }
+  }
 
   const FrameUniforms& f = a.f;
   const SceneUniforms& su = a.s;
@@ -125,7 +599,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   const uint32_t total = multi ? a.batch * ((a.npix + kChunk - 1u) / kChunk) * kChunk : a.npix;
   uint32_t chunk_frame = 0;  // wave-uniform: the frame of the wave's current chunk
   const uint32_t n_iter = iterations<ITERS>(su.n);
-  static_assert(!ANIM || (MULTI && is_mandelbulb(FAM)), "per-lane powers: multi-frame Mandelbulb launches");
+  static_assert(!ANIM || ((MULTI || RES) && is_mandelbulb(FAM)), "per-lane powers: multi-frame or ring Mandelbulb launches");
   float lane_power = su.mb_power;  // ANIM: the power of the lane's pixel's frame
   ShadeGeom* __restrict__ geom = a.geom;
   ShadeTail* __restrict__ tails = a.tails;
@@ -143,6 +617,12 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 #ifdef FRM_COUNT_EXACT
   uint64_t n_dbg_total = 0, n_dbg_exact = 0;
 #endif
+  if constexpr (RES) {
+    uint32_t b = 0;
+    if (lane == 0) b = max(a.ring.first_seq, dev_load(&a.ring.dev->base));
+    if (lane < (uint32_t)kRwWords) rw[lane] = 0u;
+    rw_set(rw, kRwSeq, uniform(__shfl(b, 0, 64)));
+  }
 
   // per-lane state
   uint32_t pix = kIdle;      // local pixel index (lr * width + x) being marched
@@ -183,7 +663,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
         if (pending == 0 || (uint32_t)__popcll(waitable & ~pending) >= a.service_min) break;
         // one body per computing lane this iteration (a DE that bails out at entry never
         // becomes pending, so this counts bodies exactly: fragment.wgsl:245-249)
-        n_body += (uint64_t)__popcll(pending);
+        if constexpr (!RES) n_body += (uint64_t)__popcll(pending);
 #ifdef FRM_STAMPS
         n_loop++;
 #endif
@@ -274,7 +754,11 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       FRM_SUB_BEGIN();
       const v3 n = normalize(nsum);
       const v3 hp = ray_at(o, t, d);
-      *reinterpret_cast<float4*>(&geom[pix]) = make_float4(t, n.x, n.y, n.z);
+      if constexpr (RES) {  // read by another wave's shading, maybe on another XCD (ring_flush)
+        coherent_store(&geom[pix], make_float4(t, n.x, n.y, n.z));
+      } else {
+        *reinterpret_cast<float4*>(&geom[pix]) = make_float4(t, n.x, n.y, n.z);
+      }
       o = shadow_origin(hp, n);
       d = to_sun();
       t = 0.f;
@@ -282,11 +766,19 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       closeness = kInfinity;
       FRM_SUB_END(2);
     }
+    if constexpr (RES) {  // count finished pixels per ring slot (ring_count_fins)
+      const uint64_t fm = ballot(fin);
+      if (fm) ring_count_fins(a, rw, fm, pix);
+    }
     if (fin) {  // primary miss (flags 0: BACKGROUND_COLOR) or end of the shadow march
       FRM_SUB_BEGIN();
       const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
       const uint32_t ck = cost_key(pix_cost);
-      *reinterpret_cast<uint2*>(&tails[pix]) = make_uint2(__float_as_uint(closeness), psteps | flags | (ck << kRecKeyShift));
+      const uint2 tail = make_uint2(__float_as_uint(closeness), psteps | flags | (ck << kRecKeyShift));
+      if constexpr (RES)
+        coherent_store(&tails[pix], tail);
+      else
+        *reinterpret_cast<uint2*>(&tails[pix]) = tail;
       pix = kIdle;
       FRM_SUB_END(3);
     }
@@ -299,6 +791,9 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     if (want != 0 && !exhausted) {
       if (slots_used == kChunk) {
         uint32_t base = kIdle;
+        if constexpr (RES) {
+          base = ring_claim(a, rw, cam_lds, drained, part, nchunks, nhead);
+        } else {
         // the head of the order (its most expensive chunks) from the shared counter
         if (!(drained >> kQueueParts)) {
           uint32_t j = 0;
@@ -325,6 +820,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           do part = (part + 1u) % kQueueParts;
           while ((drained >> part) & 1u);
         }
+        }  // !RES
 #ifdef FRM_STAMPS
         n_fetch++;
 #endif
@@ -347,15 +843,17 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
             lim = a.npix;
           }
           if (pos0 + lane < lim) {
-            const uint32_t lp = a.pixel_order[pos0 + lane];
+            const uint32_t lp = RES ? a.ring.order[rw_get(rw, kRwSlot) * a.rec_stride + pos0 + lane] : a.pixel_order[pos0 + lane];
             const uint32_t lr = lp / f.width, x = lp - lr * f.width, y = band_row_to_global(a.g, lr);
-            if constexpr (multi)
+            if constexpr (RES)
+              ray = camera_ray_rows(f, *reinterpret_cast<const float(*)[3][4]>(cam_lds), x, y);
+            else if constexpr (multi)
               ray = camera_ray_rows(f, a.cams[chunk_frame].row, x, y);
             else
               ray = camera_ray(f, x, y);
-            p = chunk_frame * a.rec_stride + lp;  // the pixel's record index
+            p = (RES ? rw_get(rw, kRwSlot) * a.rec_stride : chunk_frame * a.rec_stride) + lp;  // the pixel's record index
           }
-          n_pix += count(p != kIdle);
+          if constexpr (!RES) n_pix += count(p != kIdle);
           chunk_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
           __builtin_amdgcn_wave_barrier();
           slots_used = 0;
@@ -369,8 +867,14 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           if (pix != kIdle) {
             pix_cost = 0;
             d = mk(r.x, r.y, r.z);
-            o = multi ? a.cams[chunk_frame].origin : f.origin;
-            if constexpr (ANIM) lane_power = a.mb_powers[chunk_frame];
+            if constexpr (RES)
+              o = mk(cam_lds[12], cam_lds[13], cam_lds[14]);
+            else
+              o = multi ? a.cams[chunk_frame].origin : f.origin;
+            if constexpr (RES && ANIM)
+              lane_power = cam_lds[15];
+            else if constexpr (ANIM)
+              lane_power = a.mb_powers[chunk_frame];
             t = 0.f;
             it = 0;
             phase = kPrimary;
@@ -408,16 +912,25 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       }
     }
 
-    n_prim += count(ev_prim);
-    n_hit += count(ev_hit);
-    n_shadow += count(ev_shadow);
-    n_bail += count(ev_bail);
+    // work counters (frm_stats); a ring grid's frames report none (frm_render with stats renders
+    // outside the ring), so it keeps no counters
+    if constexpr (!RES) {
+      n_prim += count(ev_prim);
+      n_hit += count(ev_hit);
+      n_shadow += count(ev_shadow);
+      n_bail += count(ev_bail);
+    }
 #ifdef FRM_STAMPS
     stamp_service += __builtin_amdgcn_s_memtime() - stamp0;
     n_service++;
 #endif
 
     if (exhausted && ballot(pix != kIdle) == 0) break;
+  }
+  if constexpr (RES) {
+#pragma unroll
+    for (uint32_t sl = 0; sl < kRingSlots; ++sl)
+      if (sl < a.ring.slots) ring_flush(a, rw, sl);
   }
 
 #ifdef FRM_STAMPS
@@ -449,7 +962,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
     }
   }
 #endif
-  if (lane == 0) {
+  if (lane == 0 && !RES) {
 #ifdef FRM_COUNT_EXACT
     atomicAdd(&a.counters[7], (unsigned long long)((n_dbg_total << 32) | n_dbg_exact));
 #endif
