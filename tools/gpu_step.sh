@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session steps: run the given steps in order, each under its own time limit; stop at the
 # first step that ends in anything but success or ordinary test failures (rc 0/1/3).
-# usage: tools/gpu_r5_step.sh 'SECONDS|NAME|COMMAND' ...
+# usage: tools/gpu_step.sh 'SECONDS|NAME|COMMAND' ...
 mkdir -p gpurun_out
 for spec in "$@"; do
   secs=${spec%%|*}; rest=${spec#*|}; name=${rest%%|*}; cmd=${rest#*|}
