@@ -215,7 +215,7 @@ struct frm_ctx {
   bool has_params = false;
   SceneUniforms scene{};
   Ring ring;
-  bool ring_enabled = true;  // FRM_RING=0: every frm_render launches its own grid (A/B)
+  bool ring_enabled = false;  // FRM_RING=1: the resident frame ring (opt-in: slower)
   bool last_is_ring = false; // the last frm_render posted a ring frame (ring.last_seq)
   std::string error;
 };
@@ -850,15 +850,20 @@ int ring_setup(frm_ctx* ctx) {
   RingDev* img = new (std::nothrow) RingDev();
   if (!img) return fail(ctx, FRM_ERR_OUT_OF_MEMORY, "host allocation failed");
   img->base = k0;
-  for (uint32_t s = 0; s < kRingSlots; ++s) {
-    const uint32_t seq = k0 + ((s + slots - ((k0 - 1u) & (slots - 1u))) & (slots - 1u));
+  memset(img->trace, 0xff, sizeof(img->trace));
+  memset(img->grid_trace, 0xff, sizeof(img->grid_trace));
+  for (auto& t : img->trace) t[2] = 0;  // max field
+  // the counter sets of the first `slots` frames (the later ones are set up by the frame that
+  // completes `slots` frames before them, ring_finish)
+  for (uint32_t seq = k0; seq < k0 + slots; ++seq) {
     const unsigned long long ep = (unsigned long long)seq << 32;
-    RingSlotCtl& c = img->slot[s];
+    RingFrameCtl& c = img->set[(seq - 1u) & (2u * slots - 1u)];
     for (uint32_t x = 0; x <= kQueueParts; ++x) c.queue[x * (kQueuePartWords / 2u)] = ep;
     c.pix_done[0] = c.shade_next[0] = c.shade_done[0] = c.rank_next[0] = c.rank_done[0] = ep;
-    const uint32_t prev = seq > slots ? seq - slots : 0u;
-    c.done_seq[0] = prev;
-    if (s < slots) __atomic_store_n(&R.host->done[s][0], prev, __ATOMIC_RELAXED);
+    const uint32_t s = (seq - 1u) & (slots - 1u);
+    const uint32_t prev = seq > slots ? seq - slots : 0u;  // the slot's last frame: done (quiesced)
+    img->done_seq[s][0] = prev;
+    __atomic_store_n(&R.host->done[s][0], prev, __ATOMIC_RELAXED);
   }
   const hipError_t e = hipMemcpy(R.dev, img, sizeof(RingDev), hipMemcpyHostToDevice);
   delete img;
@@ -1082,7 +1087,7 @@ static int create_one(const frm_config* config, int device, frm_ctx** out_ctx) {
   ctx->flags = config->flags;
   ctx->nslots = config->frames_in_flight ? config->frames_in_flight : 1u;
   if (const char* env = getenv("FRM_SCHED")) ctx->fused_sched = strcmp(env, "sort") != 0;
-  if (const char* env = getenv("FRM_RING")) ctx->ring_enabled = strcmp(env, "0") != 0;  // A/B: per-frame grids
+  if (const char* env = getenv("FRM_RING")) ctx->ring_enabled = strcmp(env, "0") != 0;  // opt-in ring
   if (const char* env = getenv("FRM_RING_SERVICE")) {  // service waves of a ring grid (tuning)
     long v = strtol(env, nullptr, 10);
     if (v >= 1 && v <= 1024) ctx->ring.service_waves = (uint32_t)v;
@@ -1242,6 +1247,29 @@ int frm_destroy(frm_ctx* ctx) {
   {
     Ring& R = ctx->ring;
     if (R.grid_id) (void)ring_quiesce(ctx);
+    if (getenv("FRM_RING_DEBUG")) {
+      fprintf(stderr, "frm ring: %u frames posted, %u grids launched, %u service waves\n", R.last_seq, R.grid_id,
+              R.service_waves);
+      // FRM_RING_TRACE builds: the device timeline of the last frames (us from the first event shown)
+      RingDev* d = R.dev ? new (std::nothrow) RingDev() : nullptr;
+      if (d && hipMemcpy(d, R.dev, sizeof(RingDev), hipMemcpyDeviceToHost) == hipSuccess && d->trace[1][1] &&
+          d->trace[1][1] != ~0ull) {
+        const uint32_t first = R.last_seq > 40u ? R.last_seq - 40u : 1u;
+        const unsigned long long t0 = d->trace[first & 63u][0];
+        for (uint32_t q = first; q <= R.last_seq; ++q) {
+          const unsigned long long* t = d->trace[q & 63u];
+          fprintf(stderr, "frm ring trace: frame %u seen %.1f claims %.1f..%.1f marched %.1f shaded %.1f done %.1f\n", q,
+                  (double)(long long)(t[0] - t0) / 100.0, (double)(long long)(t[1] - t0) / 100.0,
+                  (double)(long long)(t[2] - t0) / 100.0, (double)(long long)(t[3] - t0) / 100.0,
+                  (double)(long long)(t[4] - t0) / 100.0, (double)(long long)(t[5] - t0) / 100.0);
+        }
+        for (uint32_t id = R.grid_id > 30u ? R.grid_id - 30u : 1u; id <= R.grid_id; ++id)
+          fprintf(stderr, "frm ring trace: grid %u start %.1f close %.1f\n", id,
+                  (double)(long long)(d->grid_trace[id & 63u][0] - t0) / 100.0,
+                  (double)(long long)(d->grid_trace[id & 63u][1] - t0) / 100.0);
+      }
+      delete d;
+    }
     ring_free_buffers(R);
     ring_free_images(R);
     for (const Ring::Retired& r : R.retired) (void)hipHostFree(r.img);

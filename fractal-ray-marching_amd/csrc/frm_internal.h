@@ -84,7 +84,7 @@ constexpr uint32_t kShadeBlockPixels = 4096;  // shade_pass / rank_pass: local p
 // (g - 1) % slots. The host posts frame g only after frame g - slots is done (its slot is free).
 constexpr uint32_t kRingSlots = 4;
 constexpr uint32_t kRingGridIds = 8;  // RingHost::grid_stop entries (grid id % 8)
-constexpr uint32_t kRingRankPixels = 1024;  // local pixels per rank task (16 per lane)
+constexpr uint32_t kRingTaskPixels = 16384;  // local pixels per shade or rank task (256 per lane)
 
 // One posted frame (pinned host memory; the host writes it before it posts the frame, the
 // device reads it with system-scope loads).
@@ -110,11 +110,13 @@ struct RingHost {
   RingFrame frames[kRingSlots];
 };
 
-// Per-slot device state. The claim and completion counters are 64-bit words whose high half is
-// the seq of the frame they count (an "epoch"): the frame that completes a slot writes the next
-// frame's epoch (seq + slots) with a zero count, so a late or stale atomic of an earlier frame
-// sees a foreign epoch and does nothing. Each word sits in its own 256-byte line.
-struct RingSlotCtl {
+// Per-frame device state: the claim and completion counters of one frame, in one of 2 x slots
+// sets (frame g: set (g - 1) % (2 R)). Each counter is a 64-bit word whose high half is the seq of
+// the frame it counts (an "epoch"). The frame that completes writes the set of frame g + R (last used
+// by frame g - R, done before g was posted) with that frame's epoch and zero counts, so an atomic
+// that arrives late for a finished frame lands on a set nobody reuses for another frame's length,
+// and one that meets a foreign epoch is recognised. Each word sits in its own 256-byte line.
+struct RingFrameCtl {
   unsigned long long queue[(kQueueParts + 1u) * (kQueuePartWords / 2u)];  // claim counters: partition x at
                                                                           // x * 32, the head at kQueueParts * 32
   unsigned long long pix_done[32];    // local pixels whose march has ended
@@ -123,8 +125,8 @@ struct RingSlotCtl {
   unsigned long long rank_next[32];   // rank tasks claimed
   unsigned long long rank_done[32];   // rank tasks done
   uint32_t hist[kRankWords];          // cost-key histogram (256) + rank cursors (256)
-  uint32_t done_seq[64];              // the slot's last completed frame (device copy of RingHost::done)
 };
+constexpr uint32_t kRingSets = 2u * kRingSlots;
 
 struct RingGridCtl {  // per grid launch (zeroed before it)
   uint32_t closed, limit, limit_valid, pad[61];
@@ -134,7 +136,12 @@ struct RingDev {  // device memory, per context
   uint32_t base;  // the first seq the next grid serves (its predecessor's last + 1)
   uint32_t pad[63];
   RingGridCtl grid;
-  RingSlotCtl slot[kRingSlots];
+  uint32_t done_seq[kRingSlots][64];  // per slot: its last completed frame (device copy of RingHost::done)
+  RingFrameCtl set[kRingSets];
+  // FRM_RING_TRACE builds: per frame (seq % 64) the 100 MHz device time of its first posting seen,
+  // first claim, last claim, march end, shading end, completion; per grid (id % 64) start and close
+  unsigned long long trace[64][8];
+  unsigned long long grid_trace[64][4];
 };
 
 // A grid's view of the ring (KernelArgs::ring).

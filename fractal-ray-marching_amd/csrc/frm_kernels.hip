@@ -245,6 +245,7 @@ static hipError_t launch_ring_fam(const KernelArgs& args, int cu_count, hipStrea
   if (const int v = blocks_override()) bpc = v;
   const uint32_t blocks = (uint32_t)(bpc * cu_count);
   if (out_blocks) *out_blocks = (int)blocks;
+  if (getenv("FRM_RING_DEBUG")) fprintf(stderr, "frm ring grid: %d blocks per CU (occupancy %d), %u blocks\n", bpc, blocks_per_cu, blocks);
   if (args.ring.service_waves >= blocks) return hipErrorInvalidValue;
   hipLaunchKernelGGL((march_persistent<FAM, ITERS, false, kAnim, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
   return hipGetLastError();

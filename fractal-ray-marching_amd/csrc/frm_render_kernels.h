@@ -96,67 +96,97 @@ __device__ __forceinline__ uint8_t cost_key(uint32_t bodies) {
 }
 
 // ---- resident frame ring: device side (frm_internal.h RingArgs) ----------------------------
+// The ring's memory is shared by waves on different XCDs, whose L2s are not coherent with each
+// other, and with the host. The rules the code below follows:
+//  * counters and flags are only touched by atomics, which are performed at the coherence point;
+//    a poll is an atomic fetch (never a load that an acquire would have to make fresh: an acquire
+//    invalidates the wave's whole L2, and polling with acquire loads ran the ring 3.5x slower);
+//  * data one wave writes for another (records, cost keys, fetch orders) is stored with agent-scope
+//    stores, which write through the L2, and the writer waits for its stores (ring_wait_mem) before
+//    the atomic that publishes them;
+//  * such data is read with agent-scope loads, which never return a stale line of the reader's
+//    XCD L2 (an acquire fence instead invalidates that whole L2: one per shade/rank task and per
+//    frame a march wave entered, ~10^4 per frame, slowed every wave on the XCD);
+//  * host memory (RingHost: posted, descriptors; zero-copy images) is uncached: system-scope loads
+//    and stores, ordered by waiting.
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint32_t dev_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+template <class T>
+__device__ __forceinline__ T dev_poll(T* p) {
+  return __hip_atomic_fetch_add(p, (T)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ unsigned long long dev_load64(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+template <class T>
+__device__ __forceinline__ T dev_load(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void dev_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+template <class T>
+__device__ __forceinline__ void dev_store(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Waits until this wave's memory accesses so far have completed.
+__device__ __forceinline__ void ring_wait_mem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 constexpr uint64_t kRingWatchdogTicks = 200000000ull;  // 2 s of the 100 MHz clock without progress
 constexpr unsigned long long kEpochMask = 0xFFFFFFFF00000000ull;
 __device__ __forceinline__ unsigned long long epoch_of(uint32_t seq) { return (unsigned long long)seq << 32; }
+#ifdef FRM_RING_TRACE
+#define RING_TRACE_MIN(r, seq, k) atomicMin(&(r).dev->trace[(seq) & 63u][k], (unsigned long long)realtime())
+#define RING_TRACE_MAX(r, seq, k) atomicMax(&(r).dev->trace[(seq) & 63u][k], (unsigned long long)realtime())
+#define RING_GRID_TRACE(r, k) atomicMin(&(r).dev->grid_trace[(r).grid_id & 63u][k], (unsigned long long)realtime())
+#else
+#define RING_TRACE_MIN(r, seq, k)
+#define RING_TRACE_MAX(r, seq, k)
+#define RING_GRID_TRACE(r, k)
+#endif
+__device__ __forceinline__ RingFrameCtl& ring_ctl(const RingArgs& r, uint32_t seq) {
+  return r.dev->set[(seq - 1u) & (2u * r.slots - 1u)];
+}
+// The ring arguments a march wave needs, kept in LDS and read (volatile) where they are used: held
+// in kernel-argument SGPRs for the whole march loop they pushed its SGPRs into VGPR lanes and those
+// into scratch, reloaded on every service pass (the ring ran at 60 % of the batched march's rate).
+struct RingLds {
+  RingHost* host;
+  RingDev* dev;
+  uint32_t* order;
+  uint32_t slots, grid_id, rec_stride, npix;
+};
+__device__ __forceinline__ uint32_t rl_u32(const volatile uint32_t& v) { return uniform(v); }
+template <class T>
+__device__ __forceinline__ T* rl_ptr(T* const volatile& v) {
+  const uint64_t x = reinterpret_cast<uint64_t>(v);
+  return reinterpret_cast<T*>((uint64_t)uniform((uint32_t)x) | ((uint64_t)uniform((uint32_t)(x >> 32)) << 32));
+}
+// The march-path view of the ring arguments (see RingLds), fields read at this point.
+__device__ __forceinline__ RingArgs ring_view(const volatile RingLds* rl) {
+  RingArgs r;
+  r.host = rl_ptr(rl->host);
+  r.dev = rl_ptr(rl->dev);
+  r.order = rl_ptr(rl->order);
+  r.slots = rl_u32(rl->slots);
+  r.grid_id = rl_u32(rl->grid_id);
+  r.first_seq = 0;
+  r.service_waves = 0;
+  r.out = nullptr;
+  r.keys = nullptr;
+  return r;
+}
 
-// Lane 0's 64-bit atomic add of `v` to an epoch-tagged counter (one lane: a vector atomic),
-// broadcast: the count before the add when the word still counts frame `seq`, else ~0u.
+// Lane 0 adds v to an epoch-tagged counter of frame `seq` (frm_internal.h RingFrameCtl); broadcast:
+// the count before the add, or ~0u when the word counts another frame.
 __device__ __forceinline__ uint32_t epoch_add(unsigned long long* w, uint32_t seq, uint32_t v) {
   unsigned long long old = 0;
-  if ((threadIdx.x & 63u) == 0) {
-    // a word that already counts another frame is left alone (frm_internal.h RingSlotCtl)
-    const unsigned long long cur = dev_load64(w);
-    old = (cur & kEpochMask) == epoch_of(seq) ? atomicAdd(w, (unsigned long long)v) : cur;
-  }
+  if ((threadIdx.x & 63u) == 0) old = atomicAdd(w, (unsigned long long)v);
   old = __shfl(old, 0, 64);
   return (old & kEpochMask) == epoch_of(seq) ? (uint32_t)old : 0xFFFFFFFFu;
 }
-
-// epoch_add for a claim counter of `n` items: no atomic once the word counts n or more (or another
-// frame), so claims that find the counter exhausted leave it alone; ~0u when nothing was claimed.
-__device__ __forceinline__ uint32_t epoch_add_below(unsigned long long* w, uint32_t seq, uint32_t n) {
-  unsigned long long old = 0;
-  if ((threadIdx.x & 63u) == 0) {
-    const unsigned long long cur = dev_load64(w);
-    old = ((cur & kEpochMask) == epoch_of(seq) && (uint32_t)cur < n) ? atomicAdd(w, 1ull) : ~0ull;
-  }
-  old = __shfl(old, 0, 64);
-  return (old & kEpochMask) == epoch_of(seq) && (uint32_t)old < n ? (uint32_t)old : 0xFFFFFFFFu;
-}
-// A task claim that never moves a counter past n: compare-and-swap from a count below n. Once every
-// task of a frame is claimed no claim touches the word again, so the frame's completion (which
-// resets the word for the slot's next frame) cannot race with a late claim.
+// A claim of one of n items: its index, or ~0u (all claimed, or another frame's counter).
 __device__ __forceinline__ uint32_t epoch_claim(unsigned long long* w, uint32_t seq, uint32_t n) {
-  uint32_t got = 0xFFFFFFFFu;
-  if ((threadIdx.x & 63u) == 0) {
-    unsigned long long cur = dev_load64(w);
-    while ((cur & kEpochMask) == epoch_of(seq) && (uint32_t)cur < n) {
-      const unsigned long long prev = atomicCAS(w, cur, cur + 1ull);
-      if (prev == cur) {
-        got = (uint32_t)cur;
-        break;
-      }
-      cur = prev;
-    }
-  }
-  return uniform(__shfl(got, 0, 64));
+  const uint32_t t = epoch_add(w, seq, 1u);
+  return t < n ? t : 0xFFFFFFFFu;
 }
 
 // The frames a grid may serve: those up to min(posted, grid_stop - 1), and after the grid has
@@ -169,55 +199,61 @@ __device__ __forceinline__ void ring_refresh(const RingArgs& r, RingView& v) {
   if (v.closed) return;
   uint32_t lim = 0, closed = 0;
   if ((threadIdx.x & 63u) == 0) {
-    closed = dev_load(&r.dev->grid.limit_valid);
+    closed = dev_poll(&r.dev->grid.limit_valid);
     if (closed) {
-      lim = dev_load(&r.dev->grid.limit);
+      lim = dev_poll(&r.dev->grid.limit);
     } else {
       const uint32_t posted = sys_load(&r.host->posted);
       const uint32_t stop = sys_load(&r.host->grid_stop[r.grid_id % kRingGridIds][0]);
       lim = min(posted, stop - 1u);
+#ifdef FRM_RING_TRACE
+      if (lim >= 1u) RING_TRACE_MIN(r, lim, 0);
+#endif
     }
   }
   v.closed = uniform(__shfl(closed, 0, 64)) != 0;
   v.limit = uniform(__shfl(lim, 0, 64));
 }
 // A march wave with nothing left to claim up to v.limit closes the grid: the first to get there
-// publishes (to the host, then after a system-scope fence reads `posted` once more) the last frame
-// the grid serves; every other wave waits for that limit. Frames posted later belong to the next
-// grid, which the host launches when it sees `closed` (frm_api.hip resident_render).
+// publishes `closed` to the host, waits for that store, reads `posted` once more and fixes the last
+// frame the grid serves; every other wave waits for that limit. Frames posted later belong to the
+// next grid, which the host launches when it sees `closed` after its own post (frm_api.hip
+// ring_render: each side stores, then loads the other's word, so one of them sees the other's store).
 __device__ __forceinline__ void ring_close(const RingArgs& r, RingView& v) {
   uint32_t lim = 0, ok = 1;
   if ((threadIdx.x & 63u) == 0) {
     if (atomicCAS(&r.dev->grid.closed, 0u, 1u) == 0u) {
       sys_store(&r.host->closed, r.grid_id);
-      __atomic_thread_fence(__ATOMIC_SEQ_CST);  // system scope: the store above before the loads below
+      RING_GRID_TRACE(r, 1);
+      ring_wait_mem();
       const uint32_t posted = sys_load(&r.host->posted);
       const uint32_t stop = sys_load(&r.host->grid_stop[r.grid_id % kRingGridIds][0]);
       lim = min(posted, stop - 1u);
-      dev_store(&r.dev->grid.limit, lim);
-      dev_store(&r.dev->base, lim + 1u);
-      dev_store(&r.dev->grid.limit_valid, 1u);
+      atomicExch(&r.dev->grid.limit, lim);
+      atomicExch(&r.dev->base, lim + 1u);
+      ring_wait_mem();
+      atomicExch(&r.dev->grid.limit_valid, 1u);
     } else {
       const uint64_t t0 = realtime();
-      while (!dev_load(&r.dev->grid.limit_valid)) {
+      while (!dev_poll(&r.dev->grid.limit_valid)) {
         if (realtime() - t0 > 1000000ull) { ok = 0; break; }  // 10 ms: the closer stalled; stop here
         __builtin_amdgcn_s_sleep(2);
       }
-      lim = dev_load(&r.dev->grid.limit);
+      lim = dev_poll(&r.dev->grid.limit);
     }
   }
   v.closed = true;
   v.limit = uniform(__shfl(ok ? lim : 0u, 0, 64));
 }
 
-// The camera of ring frame `seq` into wave-uniform registers (system-scope loads of its RingFrame).
+// The camera (and zero-copy image) of ring frame slot `slot`, from its RingFrame in host memory.
 struct RingCam {
   float row[3][4];
   v3 origin;
   float power;
   uint32_t* host_img;
 };
-// The first 16 words of ring frame `slot`'s RingFrame (camera rows, origin, power) into LDS.
+// The first 16 words of the RingFrame (camera rows, origin, power) into LDS (march waves).
 __device__ __forceinline__ void ring_camera_lds(const RingArgs& r, uint32_t slot, float* lds) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&r.host->frames[slot]);
   const uint32_t lane = threadIdx.x & 63u;
@@ -239,117 +275,180 @@ __device__ __forceinline__ RingCam ring_camera(const RingArgs& r, uint32_t slot)
   return c;
 }
 
-// A ring march wave's claim state, in LDS (its SGPRs are the march's): the frame it claims from,
-// the frame of its last claimed chunk (slot), the grid's frames as it last saw them, and per slot the
-// pixels whose march ended in this wave and that the slot's pix_done does not count yet. Those are
-// added when the wave claims a chunk of that frame (it then still holds unfinished pixels of it) or
-// once it has moved past the frame (it never claims from it again), so a frame's count completes
-// only after every wave is done claiming from it.
-enum RingWaveWord : uint32_t { kRwSeq = 0, kRwCamSeq, kRwSlot, kRwLimit, kRwClosed, kRwPend, kRwWords = kRwPend + kRingSlots };
+// A ring march wave's claim state, all of it in LDS (SGPRs and VGPRs are the march's): the oldest
+// frame it has not drained, the grid's frames as it last saw them, and per slot the frame the slot's
+// state belongs to, its camera, its queue drain state and the pixels of that frame whose march
+// ended in this wave and that the frame's pix_done does not count yet; and the slots whose frames
+// the wave has drained. A slot's count goes out once the wave has drained the frame (it never
+// claims from it again) and none of its lanes holds a pixel of it (ring_settle), so a frame's count
+// completes only after every wave is done with it.
+enum RingWaveWord : uint32_t {
+  kRwLo = 0,       // the oldest frame the wave has not drained
+  kRwLimit,        // the grid's frames as this wave last saw them (RingView)
+  kRwClosed,
+  kRwSeqOf,        // + slot: the frame the slot's state (camera, drain state) belongs to
+  kRwPart = kRwSeqOf + kRingSlots,       // + slot: the queue partition the wave claims from
+  kRwDrainLo = kRwPart + kRingSlots,     // + slot: drained partitions (bits 0..31; bit kQueueParts: the head)
+  kRwDrainHi = kRwDrainLo + kRingSlots,  // + slot: high half
+  kRwPend = kRwDrainHi + kRingSlots,     // + slot: finished pixels not yet added to pix_done
+  kRwGone = kRwPend + kRingSlots,        // bit s: the wave has drained slot s's frame
+  kRwWords
+};
 __device__ __forceinline__ uint32_t rw_get(const uint32_t* rw, uint32_t i) { return uniform(rw[i]); }
 __device__ __forceinline__ void rw_set(uint32_t* rw, uint32_t i, uint32_t v) {
   if ((threadIdx.x & 63u) == 0) rw[i] = v;
 }
-// Records of a ring frame are read by the service waves' shading, which may run on another XCD:
-// the L2s of the XCDs are not coherent with each other, so the march writes them through to memory
-// (agent-scope stores, `sc1`) and waits for them (ring_flush) before it counts their pixels; the
-// shading's acquire of the count then invalidates its own L2 before it reads them.
+// Records of a ring frame are read by the service waves' shading, maybe on another XCD: written
+// through (agent-scope stores) and waited for (ring_add_done) before their pixels are counted, and
+// read with agent-scope loads (never from a stale line of the reader's L2).
 __device__ __forceinline__ void coherent_store(ShadeTail* p, uint2 v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v.x | ((unsigned long long)v.y << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  dev_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v.x | ((unsigned long long)v.y << 32));
 }
 __device__ __forceinline__ void coherent_store(ShadeGeom* p, float4 v) {
   unsigned long long* w = reinterpret_cast<unsigned long long*>(p);
-  __hip_atomic_store(w, (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(w + 1, (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  dev_store(w, (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32));
+  dev_store(w + 1, (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32));
 }
-
-// Adds slot sl's pending count to its frame's pix_done, after the wave's record stores have
-// completed (coherent_store: written through, so completion is visibility at agent scope).
-__device__ __forceinline__ void ring_flush(const KernelArgs& a, uint32_t* rw, uint32_t sl) {
-  const uint32_t pv = rw_get(rw, kRwPend + sl);
-  if (!pv) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const uint32_t seq = rw_get(rw, kRwCamSeq) - ((rw_get(rw, kRwSlot) - sl) & (a.ring.slots - 1u));
-  (void)epoch_add(&a.ring.dev->slot[sl].pix_done[0], seq, pv);
-  rw_set(rw, kRwPend + sl, 0u);
+__device__ __forceinline__ uint2 coherent_load(const ShadeTail* p) {
+  const unsigned long long v = dev_load(reinterpret_cast<const unsigned long long*>(p));
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
-// The pixels of finished-lane mask fm (record index pix = slot * rec_stride + local pixel) into the
-// per-slot pending counts; frames the wave has moved past are flushed at once.
-__device__ __forceinline__ void ring_count_fins(const KernelArgs& a, uint32_t* rw, uint64_t fm, uint32_t pix) {
-  const uint32_t R = a.ring.slots, rs = a.rec_stride;
-  uint32_t prev = 0;
+__device__ __forceinline__ float4 coherent_load(const ShadeGeom* p) {
+  const unsigned long long* w = reinterpret_cast<const unsigned long long*>(p);
+  const unsigned long long lo = dev_load(w), hi = dev_load(w + 1);
+  return make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)), __uint_as_float((uint32_t)hi),
+                     __uint_as_float((uint32_t)(hi >> 32)));
+}
+// Adds n finished pixels to frame seq's pix_done, after the wave's record stores have completed.
+__device__ __forceinline__ void ring_add_done(const volatile RingLds* rl, uint32_t seq, uint32_t n) {
+  ring_wait_mem();
+  const RingArgs r = ring_view(rl);
+  const uint32_t before = epoch_add(&ring_ctl(r, seq).pix_done[0], seq, n);
+#ifdef FRM_RING_TRACE
+  if (before + n == rl_u32(rl->npix) && (threadIdx.x & 63u) == 0) RING_TRACE_MIN(r, seq, 3);
+#else
+  (void)before;
+#endif
+}
+// Slot s's finished pixels into its frame's pix_done (see ring_settle).
+__device__ __forceinline__ void ring_flush(const volatile RingLds* rl, uint32_t* rw, uint32_t s) {
+  const uint32_t n = rw_get(rw, kRwPend + s);
+  if (n) {
+    ring_add_done(rl, rw_get(rw, kRwSeqOf + s), n);
+    rw_set(rw, kRwPend + s, 0u);
+  }
+}
+// A slot the wave has drained (bit s of kRwGone) whose pixels have all left its lanes (pix: the
+// lanes' pixels now) is settled: its count goes out and the bit clears, once per wave and frame.
+// (Counts added at every claim and every finished pixel of a drained frame were an atomic on one
+// word per service pass of every wave, each behind a wait for the wave's stores: the ring marched
+// at 60 % of the batched rate.)
+__device__ __forceinline__ void ring_settle(const volatile RingLds* rl, uint32_t* rw, uint32_t gone, uint32_t pix) {
+  const uint32_t rs = rl_u32(rl->rec_stride);
 #pragma unroll
   for (uint32_t sl = 0; sl < kRingSlots; ++sl) {
-    if (sl >= R) break;
-    const uint32_t cum = sl + 1u < R ? (uint32_t)__popcll(fm & ballot(pix < (sl + 1u) * rs))
-                                     : (uint32_t)__popcll(fm);
-    if (cum != prev) rw_set(rw, kRwPend + sl, rw_get(rw, kRwPend + sl) + (cum - prev));
-    prev = cum;
+    if (!((gone >> sl) & 1u) || ballot(pix - sl * rs < rs) != 0) continue;
+    ring_flush(rl, rw, sl);
+    rw_set(rw, kRwGone, rw_get(rw, kRwGone) & ~(1u << sl));
   }
-  const uint32_t rslot = rw_get(rw, kRwSlot);
-  const bool moved = rw_get(rw, kRwSeq) != rw_get(rw, kRwCamSeq);
-#pragma unroll
-  for (uint32_t sl = 0; sl < kRingSlots; ++sl)
-    if (sl < R && (sl != rslot || moved)) ring_flush(a, rw, sl);
 }
-// The next chunk for a ring march wave: the oldest of the grid's frames with chunks left. Returns
-// the chunk's first fetch position (kIdle: nothing left for this grid); the frame's slot in
-// rw[kRwSlot] and its camera in cam_lds. `drained`/`part` as in the single-frame claim.
-__device__ __forceinline__ uint32_t ring_claim(const KernelArgs& a, uint32_t* rw, float* cam_lds, uint64_t& drained,
-                                               uint32_t& part, uint32_t nchunks, uint32_t nhead) {
-  const uint32_t R = a.ring.slots;
+// The slot of a record index (slot * rec_stride + local pixel; at most kRingSlots slots).
+__device__ __forceinline__ uint32_t ring_slot_of(uint32_t pix, uint32_t rs) {
+  return (uint32_t)(pix >= rs) + (uint32_t)(pix >= 2u * rs) + (uint32_t)(pix >= 3u * rs);
+}
+// One claim from frame seq's queue (slot s): the head of its order first, then the partitions, as
+// the single-frame claim. Returns the chunk's first fetch position or kIdle (drained for this wave).
+__device__ __forceinline__ uint32_t ring_claim_frame(const RingArgs& r, uint32_t* rw, uint32_t seq, uint32_t s,
+                                                     uint32_t nchunks, uint32_t nhead) {
+  unsigned long long* q = ring_ctl(r, seq).queue;
+  constexpr uint32_t kW = kQueuePartWords / 2u;
+  uint64_t drained = (uint64_t)rw_get(rw, kRwDrainLo + s) | ((uint64_t)rw_get(rw, kRwDrainHi + s) << 32);
+  uint32_t part = rw_get(rw, kRwPart + s);
+  uint32_t base = kIdle;
+  if (!(drained >> kQueueParts)) {
+    const uint32_t j = epoch_claim(q + kQueueParts * kW, seq, nhead);
+    if (j != kIdle)
+      base = j * kChunk;
+    else
+      drained |= 1ull << kQueueParts;
+  }
+  while (base == kIdle) {
+    // partition `part` holds chunks nhead + j * kQueueParts + part below nchunks
+    const uint32_t jmax = nchunks > nhead + part ? (nchunks - nhead - part + kQueueParts - 1u) / kQueueParts : 0u;
+    const uint32_t j = jmax ? epoch_claim(q + part * kW, seq, jmax) : kIdle;
+    if (j != kIdle) {
+      base = (nhead + j * kQueueParts + part) * kChunk;
+      break;
+    }
+    drained |= 1ull << part;
+    if ((drained & ((1ull << kQueueParts) - 1ull)) == (1ull << kQueueParts) - 1ull) break;
+    do part = (part + 1u) % kQueueParts;
+    while ((drained >> part) & 1u);
+  }
+  rw_set(rw, kRwDrainLo + s, (uint32_t)drained);
+  rw_set(rw, kRwDrainHi + s, (uint32_t)(drained >> 32));
+  rw_set(rw, kRwPart + s, part);
+  return base;
+}
+// The claim's rare steps, as calls (inlined, their registers pushed the march state into scratch):
+// a new look at the grid's frames (and closing it), and the wave's first claim from a frame.
+__device__ __noinline__ void ring_update_view(const volatile RingLds* rl, uint32_t* rw, uint32_t lo) {
+  const RingArgs r = ring_view(rl);
+  RingView v = {rw_get(rw, kRwLimit), rw_get(rw, kRwClosed) != 0};
+  ring_refresh(r, v);
+  if (lo > v.limit && !v.closed) ring_close(r, v);
+  rw_set(rw, kRwLimit, v.limit);
+  rw_set(rw, kRwClosed, v.closed ? 1u : 0u);
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __noinline__ void ring_enter_frame(const volatile RingLds* rl, uint32_t* rw, float* cam, uint32_t s,
+                                              uint32_t f) {
+  const RingArgs r = ring_view(rl);
+  ring_camera_lds(r, s, cam);
+  rw_set(rw, kRwSeqOf + s, f);
+  rw_set(rw, kRwDrainLo + s, 0u);
+  rw_set(rw, kRwDrainHi + s, 0u);
+  rw_set(rw, kRwPart + s, queue_part());
+  __builtin_amdgcn_wave_barrier();
+}
+// The next chunk for a ring march wave. Returns the chunk's first fetch position (kIdle: nothing
+// left for this grid) and its slot (*out_slot); the slot's camera is in cam_lds[slot].
+// Frames in posting order: the wave claims from the oldest frame it has not drained and moves on
+// when that frame's queue is empty for it. Each frame's claims thus end while the next frame still
+// has most of its chunks, so the frame completes (is shaded and published, its slot freed) while
+// the grid marches the next one, and the host posts the frame after that before the grid runs
+// dry: with two slots the grid never closes in a steady loop. (Round-robin claims over the posted
+// frames drained two frames together, as a 2-frame multi-frame launch: the grid then closed after
+// every pair and paid a drain per pair; measured no faster.)
+__device__ __forceinline__ uint32_t ring_claim(const volatile RingLds* rl, uint32_t* rw, float (*cam_lds)[16],
+                                               uint32_t nchunks, uint32_t nhead, uint32_t pix, uint32_t* out_slot) {
+  const uint32_t R = rl_u32(rl->slots);
   for (;;) {
-    uint32_t seq = rw_get(rw, kRwSeq);
-    if (seq > rw_get(rw, kRwLimit)) {
-      RingView v = {rw_get(rw, kRwLimit), rw_get(rw, kRwClosed) != 0};
-      ring_refresh(a.ring, v);
-      if (seq > v.limit && !v.closed) ring_close(a.ring, v);
-      rw_set(rw, kRwLimit, v.limit);
-      rw_set(rw, kRwClosed, v.closed ? 1u : 0u);
-      if (seq > v.limit) return kIdle;  // nothing left for this grid
+    const uint32_t f = rw_get(rw, kRwLo);
+    if (f > rw_get(rw, kRwLimit)) {
+      ring_update_view(rl, rw, f);
+      if (f > rw_get(rw, kRwLimit)) return kIdle;  // nothing left for this grid
     }
-    if (seq != rw_get(rw, kRwCamSeq)) {  // a frame this wave has not claimed from yet
-      const uint32_t slot = (seq - 1u) & (R - 1u);
-      ring_camera_lds(a.ring, slot, cam_lds);
-      rw_set(rw, kRwSlot, slot);
-      rw_set(rw, kRwCamSeq, seq);
-      drained = 0;
-      part = queue_part();
+    const uint32_t s = (f - 1u) & (R - 1u);
+    if (rw_get(rw, kRwSeqOf + s) != f) {  // the wave's first claim from frame f
+      ring_enter_frame(rl, rw, cam_lds[s], s, f);
+      rw_set(rw, kRwGone, rw_get(rw, kRwGone) & ~(1u << s));
     }
-    const uint32_t slot = rw_get(rw, kRwSlot);
-    unsigned long long* q = a.ring.dev->slot[slot].queue;
-    constexpr uint32_t kW = kQueuePartWords / 2u;
-    uint32_t base = kIdle;
-    if (!(drained >> kQueueParts)) {
-      const uint32_t j = epoch_add_below(q + kQueueParts * kW, seq, nhead);
-      if (j < nhead)
-        base = j * kChunk;
-      else
-        drained |= 1ull << kQueueParts;
-    }
-    while (base == kIdle) {
-      // partition `part` holds chunks nhead + j * kQueueParts + part below nchunks
-      const uint32_t jmax = nchunks > nhead + part ? (nchunks - nhead - part + kQueueParts - 1u) / kQueueParts : 0u;
-      const uint32_t j = epoch_add_below(q + part * kW, seq, jmax);
-      const uint32_t c = j == kIdle ? nchunks : nhead + j * kQueueParts + part;
-      if (c < nchunks) {
-        base = c * kChunk;
-        break;
-      }
-      drained |= 1ull << part;
-      if ((drained & ((1ull << kQueueParts) - 1ull)) == (1ull << kQueueParts) - 1ull) break;
-      do part = (part + 1u) % kQueueParts;
-      while ((drained >> part) & 1u);
-    }
+    const RingArgs r = ring_view(rl);
+    const uint32_t base = ring_claim_frame(r, rw, f, s, nchunks, nhead);
     if (base != kIdle) {
-      ring_flush(a, rw, slot);  // the wave holds unfinished pixels of this frame: its count stays short
+#ifdef FRM_RING_TRACE
+      if ((threadIdx.x & 63u) == 0) {
+        RING_TRACE_MIN(r, f, 1);
+        RING_TRACE_MAX(r, f, 2);
+      }
+#endif
+      *out_slot = s;
       return base;
     }
-    rw_set(rw, kRwSeq, seq + 1u);  // drained for this wave: it never claims from that frame again
-    ring_flush(a, rw, slot);
+    rw_set(rw, kRwGone, rw_get(rw, kRwGone) | (1u << s));  // drained for this wave: it never claims from frame f again
+    ring_settle(rl, rw, 1u << s, pix);
+    rw_set(rw, kRwLo, f + 1u);
   }
 }
 
@@ -365,30 +464,30 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v) {
   return inc - v;
 }
 
-// Shade task t of ring frame `seq` (slot s): kShadeBlockPixels local pixels, 64 at a time, as
+// Shade task t of ring frame `seq` (slot s): kRingTaskPixels local pixels, 64 at a time, as
 // shade_pass (fragment.wgsl:333-348 + the Rgba8UnormSrgb store) with the frame's ring camera; the
 // cost keys go out for the slot's next fetch order and into the frame's key histogram.
 template <uint32_t FAM>
-__device__ void ring_shade_task(const KernelArgs& a, const RingCam& cam, uint32_t s, uint32_t t,
+__device__ void ring_shade_task(const KernelArgs& a, const RingCam& cam, uint32_t seq, uint32_t s, uint32_t t,
                                 const float* table, uint32_t* cnt) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t width = a.f.width, npix = a.npix, rs = a.rec_stride;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) cnt[lane * 4u + k] = 0u;
   __syncthreads();  // one-wave workgroup: orders the LDS accesses
-  for (uint32_t j = 0; j < kShadeBlockPixels / 64u; ++j) {
-    const uint32_t idx = t * kShadeBlockPixels + j * 64u + lane;
+  for (uint32_t j = 0; j < kRingTaskPixels / 64u; ++j) {
+    const uint32_t idx = t * kRingTaskPixels + j * 64u + lane;
     if (idx >= npix) break;
     const uint32_t lr = idx / width, x = idx - lr * width;
     const uint32_t y = band_row_to_global(a.g, lr);
     const uint32_t rec = s * rs + idx;
-    const uint2 r1 = *reinterpret_cast<const uint2*>(&a.tails[rec]);
+    const uint2 r1 = coherent_load(&a.tails[rec]);
     const uint32_t key = r1.y >> kRecKeyShift;
-    a.ring.keys[rec] = (uint8_t)key;
+    dev_store(&a.ring.keys[rec], (uint8_t)key);
     atomicAdd(&cnt[key], 1u);
     uint32_t word = 255u << 24;  // miss: BACKGROUND_COLOR
     if (r1.y & kRecHit) {
-      const float4 r0 = *reinterpret_cast<const float4*>(&a.geom[rec]);
+      const float4 r0 = coherent_load(&a.geom[rec]);
       const v3 dir = camera_ray_rows(a.f, cam.row, x, y);
       const v3 hp = ray_at(cam.origin, r0.x, dir);
       const v3 n = mk(r0.y, r0.z, r0.w);
@@ -401,30 +500,29 @@ __device__ void ring_shade_task(const KernelArgs& a, const RingCam& cam, uint32_
     if (cam.host_img) cam.host_img[idx] = word;  // zero-copy readback (pinned host image)
   }
   __syncthreads();
-  uint32_t* hist = a.ring.dev->slot[s].hist;
+  uint32_t* hist = ring_ctl(a.ring, seq).hist;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k)
     if (const uint32_t c = cnt[lane * 4u + k]) atomicAdd(&hist[lane * 4u + k], c);
 }
 
-// Rank task t of ring frame `seq` (slot s): kRingRankPixels local pixels into the slot's next fetch
+// Rank task t of ring frame `seq` (slot s): kRingTaskPixels local pixels into the slot's next fetch
 // order, by descending cost key (rank_pass's counting sort: bucket bases from the frame's complete
-// histogram, a range per task and key reserved through the cursors hist[256..511]; each pixel's
-// place in its range from an LDS atomic). Placement only: never a pixel's bytes.
-__device__ __forceinline__ void ring_rank_task(const KernelArgs& a, uint32_t s, uint32_t t, uint32_t* cnt,
-                                               uint32_t* base) {
-  constexpr uint32_t kPer = kRingRankPixels / 64u;
+// histogram, a range per task and key reserved through the cursors hist[256..511]; a pixel's place in
+// its range from an LDS atomic on a second pass over the keys). Placement only: never a pixel's bytes.
+__device__ __forceinline__ void ring_rank_task(const KernelArgs& a, uint32_t seq, uint32_t s, uint32_t t,
+                                               uint32_t* cnt) {
   const uint32_t lane = threadIdx.x & 63u, npix = a.npix, rs = a.rec_stride;
   const uint8_t* keys = a.ring.keys + (size_t)s * rs;
   uint32_t* order = a.ring.order + (size_t)s * rs;
-  uint32_t* hist = a.ring.dev->slot[s].hist;
+  uint32_t* hist = ring_ctl(a.ring, seq).hist;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) cnt[lane * 4u + k] = 0u;
   __syncthreads();
-#pragma unroll
-  for (uint32_t j = 0; j < kPer; ++j) {
-    const uint32_t idx = t * kRingRankPixels + j * 64u + lane;
-    if (idx < npix) atomicAdd(&cnt[keys[idx]], 1u);
+  for (uint32_t j = 0; j < kRingTaskPixels / 64u; ++j) {
+    const uint32_t idx = t * kRingTaskPixels + j * 64u + lane;
+    if (idx >= npix) break;
+    atomicAdd(&cnt[dev_load(&keys[idx])], 1u);
   }
   __syncthreads();
   // descending key order: lane l holds keys 255 - 4l .. 252 - 4l; base[k] = pixels with a key above
@@ -432,47 +530,59 @@ __device__ __forceinline__ void ring_rank_task(const KernelArgs& a, uint32_t s, 
   uint32_t h[4], sum = 0;
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) {
-    h[i] = hist[255u - (lane * 4u + i)];
+    h[i] = dev_load(&hist[255u - (lane * 4u + i)]);
     sum += h[i];
   }
   uint32_t before = wave_exclusive_scan(sum);
+  uint32_t b[4];
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) {
     const uint32_t k = 255u - (lane * 4u + i);
     const uint32_t c = cnt[k];
-    base[k] = before + (c ? atomicAdd(&hist[256u + k], c) : 0u);
+    b[i] = before + (c ? atomicAdd(&hist[256u + k], c) : 0u);
     before += h[i];
   }
-  __syncthreads();
+  __syncthreads();  // every lane has read its counts: the array now takes the bases
 #pragma unroll
-  for (uint32_t j = 0; j < kPer; ++j) {
-    const uint32_t idx = t * kRingRankPixels + j * 64u + lane;
-    if (idx < npix) {
-      const uint32_t pos = atomicAdd(&base[keys[idx]], 1u);
-      if (pos < npix) order[pos] = idx;  // always, for a histogram of these keys
-    }
+  for (uint32_t i = 0; i < 4; ++i) cnt[255u - (lane * 4u + i)] = b[i];
+  __syncthreads();
+  for (uint32_t j = 0; j < kRingTaskPixels / 64u; ++j) {
+    const uint32_t idx = t * kRingTaskPixels + j * 64u + lane;
+    if (idx >= npix) break;
+    const uint32_t pos = atomicAdd(&cnt[dev_load(&keys[idx])], 1u);
+    if (pos < npix) dev_store(&order[pos], idx);  // always, for a histogram of these keys
   }
 }
 
-// Every task of ring frame `seq` (slot s) is done: reset the slot for frame seq + slots (the next
-// frame's epoch on every counter, histogram and cursors zeroed), then publish the frame.
+// Every task of ring frame `seq` (slot s) is done: set up the counters of frame seq + slots (its
+// epoch, zero counts, histogram and cursors), then publish the frame.
 __device__ __forceinline__ void ring_finish(const KernelArgs& a, uint32_t seq, uint32_t s) {
   const uint32_t lane = threadIdx.x & 63u;
-  RingSlotCtl& c = a.ring.dev->slot[s];
-  const unsigned long long next = epoch_of(seq + a.ring.slots);
-  if (lane <= kQueueParts) c.queue[lane * (kQueuePartWords / 2u)] = next;
-  if (lane == 16u) c.pix_done[0] = next;
-  if (lane == 17u) c.shade_next[0] = next;
-  if (lane == 18u) c.shade_done[0] = next;
-  if (lane == 19u) c.rank_next[0] = next;
-  if (lane == 20u) c.rank_done[0] = next;
+  const uint32_t next_seq = seq + a.ring.slots;
+  RingFrameCtl& c = ring_ctl(a.ring, next_seq);
+  const unsigned long long next = epoch_of(next_seq);
+  if (lane <= kQueueParts) dev_store(&c.queue[lane * (kQueuePartWords / 2u)], next);
+  if (lane == 16u) dev_store(&c.pix_done[0], next);
+  if (lane == 17u) dev_store(&c.shade_next[0], next);
+  if (lane == 18u) dev_store(&c.shade_done[0], next);
+  if (lane == 19u) dev_store(&c.rank_next[0], next);
+  if (lane == 20u) dev_store(&c.rank_done[0], next);
 #pragma unroll
-  for (uint32_t k = 0; k < kRankWords / 64u; ++k) c.hist[k * 64u + lane] = 0u;
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);  // system scope: the reset and every shaded pixel first
+  for (uint32_t k = 0; k < kRankWords / 64u; ++k) dev_store(&c.hist[k * 64u + lane], 0u);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: before the host sees the frame done
   if (lane == 0) {
-    dev_store(&c.done_seq[0], seq);
+    RING_TRACE_MIN(a.ring, seq, 5);
+    atomicExch(&a.ring.dev->done_seq[s][0], seq);
     sys_store(&a.ring.host->done[s][0], seq);
   }
+}
+
+// An idle service wave's pause between polls, ~13 us (4 x 127 x 64 clocks): its polls are atomics at
+// the coherence point, which the march's claims and counts also go through; polling every half
+// microsecond from 128 waves slowed the march to about half its rate (128 -> 512 waves: 4x worse).
+__device__ __forceinline__ void ring_idle() {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(127);
 }
 
 // A ring grid's service wave: shades, ranks and publishes the grid's frames as their marches
@@ -480,16 +590,14 @@ __device__ __forceinline__ void ring_finish(const KernelArgs& a, uint32_t seq, u
 // every frame up to its limit is done. Sleeps between polls; gives up after kRingWatchdogTicks
 // without progress (the host then reports the frame as never completed, frm_api.hip).
 template <uint32_t FAM>
-__device__ void ring_service(const KernelArgs& a, float* table, uint32_t* cnt, uint32_t* base) {
+__device__ __noinline__ void ring_service(const KernelArgs& a, uint32_t* cnt) {
   const RingArgs& R = a.ring;
   const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) table[lane * 4u + k] = kSrgbThresholds[lane * 4u + k];
+  const float* table = kSrgbThresholds;  // (global: the service waves share the march waves' LDS budget)
   const uint32_t npix = a.npix;
-  const uint32_t nsh = (npix + kShadeBlockPixels - 1u) / kShadeBlockPixels;
-  const uint32_t nrk = (npix + kRingRankPixels - 1u) / kRingRankPixels;
+  const uint32_t ntask = (npix + kRingTaskPixels - 1u) / kRingTaskPixels;
   uint32_t seq0 = 0;
-  if (lane == 0) seq0 = max(R.first_seq, dev_load(&R.dev->base));
+  if (lane == 0) seq0 = max(R.first_seq, dev_poll(&R.dev->base));
   seq0 = uniform(__shfl(seq0, 0, 64));
   RingView rv = {0u, false};
   uint64_t last_progress = realtime();
@@ -500,24 +608,24 @@ __device__ void ring_service(const KernelArgs& a, float* table, uint32_t* cnt, u
     for (;;) {
       if (seq0 > rv.limit) break;
       uint32_t d = 0;
-      if (lane == 0) d = dev_load(&R.dev->slot[(seq0 - 1u) & (R.slots - 1u)].done_seq[0]);
+      if (lane == 0) d = dev_poll(&R.dev->done_seq[(seq0 - 1u) & (R.slots - 1u)][0]);
       if (uniform(__shfl(d, 0, 64)) < seq0) break;
       ++seq0;
     }
     if (seq0 > rv.limit) {
       if (rv.closed) return;  // every frame of this grid is done
       if (realtime() - last_progress > kRingWatchdogTicks) return;
-      __builtin_amdgcn_s_sleep(32);
+      ring_idle();
       continue;
     }
     bool worked = false;
     for (uint32_t g = seq0; g <= rv.limit && g < seq0 + R.slots && !worked; ++g) {
       const uint32_t s = (g - 1u) & (R.slots - 1u);
-      RingSlotCtl& c = R.dev->slot[s];
+      RingFrameCtl& c = ring_ctl(R, g);
       unsigned long long pd = 0, sd = 0;
       if (lane == 0) {
-        pd = dev_load64(&c.pix_done[0]);
-        sd = dev_load64(&c.shade_done[0]);
+        pd = dev_poll(&c.pix_done[0]);
+        sd = dev_poll(&c.shade_done[0]);
       }
       pd = __shfl(pd, 0, 64);
       sd = __shfl(sd, 0, 64);
@@ -526,23 +634,25 @@ __device__ void ring_service(const KernelArgs& a, float* table, uint32_t* cnt, u
         last_progress = realtime();
       }
       if (pd != (epoch_of(g) | npix)) continue;  // its march has not ended yet
-      if (sd == (epoch_of(g) | nsh)) {
-        const uint32_t t = epoch_claim(&c.rank_next[0], g, nrk);
-        if (t >= nrk) continue;
-        ring_rank_task(a, s, t, cnt, base);
-        __atomic_thread_fence(__ATOMIC_RELEASE);
-        if (epoch_add(&c.rank_done[0], g, 1u) == nrk - 1u) {
-          __atomic_thread_fence(__ATOMIC_ACQUIRE);
-          ring_finish(a, g, s);
-        }
+      if (sd == (epoch_of(g) | ntask)) {
+        const uint32_t t = epoch_claim(&c.rank_next[0], g, ntask);
+        if (t == kIdle) continue;
+        ring_rank_task(a, g, s, t, cnt);
+        ring_wait_mem();  // its order entries and cursors, before it counts as done
+        if (epoch_add(&c.rank_done[0], g, 1u) == ntask - 1u) ring_finish(a, g, s);
         worked = true;
       } else {
-        const uint32_t t = epoch_claim(&c.shade_next[0], g, nsh);
-        if (t >= nsh) continue;
+        const uint32_t t = epoch_claim(&c.shade_next[0], g, ntask);
+        if (t == kIdle) continue;
         const RingCam cam = ring_camera(R, s);
-        ring_shade_task<FAM>(a, cam, s, t, table, cnt);
-        __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the pixels (host image too) first
-        epoch_add(&c.shade_done[0], g, 1u);
+        ring_shade_task<FAM>(a, cam, g, s, t, table, cnt);
+        // its pixels, keys and histogram counts first; the zero-copy image's stores reach the host
+        // before the frame is published (a system-scope release: the image is read by the host)
+        if (cam.host_img)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        else
+          ring_wait_mem();
+        if (epoch_add(&c.shade_done[0], g, 1u) == ntask - 1u && lane == 0) RING_TRACE_MIN(R, g, 4);
         worked = true;
       }
     }
@@ -550,7 +660,7 @@ __device__ void ring_service(const KernelArgs& a, float* table, uint32_t* cnt, u
       last_progress = realtime();
     } else {
       if (realtime() - last_progress > kRingWatchdogTicks) return;
-      __builtin_amdgcn_s_sleep(16);
+      ring_idle();
     }
   }
 }
@@ -575,15 +685,24 @@ template <uint32_t FAM, bool ITERS, bool MULTI = false, bool ANIM = false, bool 
 #ifndef FRM_MARCH_WAVES_PER_SIMD
 #define FRM_MARCH_WAVES_PER_SIMD 1
 #endif
-__global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_persistent(KernelArgs a) {
+#ifndef FRM_RING_WAVES_PER_SIMD
+#define FRM_RING_WAVES_PER_SIMD FRM_MARCH_WAVES_PER_SIMD
+#endif
+__global__ __launch_bounds__(kMarchBlock, RES ? FRM_RING_WAVES_PER_SIMD : FRM_MARCH_WAVES_PER_SIMD) void march_persistent(
+    KernelArgs a) {
   __shared__ float4 chunk_rays[kMarchWaves][kChunk];  // per wave: camera ray xyz + record index bits
   static_assert(!RES || (!MULTI && kMarchWaves == 1u), "ring grids: one-wave workgroups, one frame per chunk");
-  __shared__ float cam_lds[RES ? 16 : 1];  // RES: the camera of the wave's current frame (rows, origin, power)
+  __shared__ float cam_lds[RES ? kRingSlots : 1][16];  // RES: per slot the camera of its frame (rows, origin, power)
   __shared__ uint32_t rw[RES ? (uint32_t)kRwWords : 1u];  // RES: the wave's claim state (RingWaveWord)
+  __shared__ RingLds ring_lds[RES ? 1 : 0 + 1];           // RES: the ring arguments of the march (RingLds)
   if constexpr (RES) {
-    __shared__ uint32_t svc_lds[768];  // service waves: sRGB table, key counts, bucket bases
+    // service waves: key counts / bucket bases in the LDS the march waves use for chunk rays (one
+    // workgroup is one wave: either kind)
     if (blockIdx.x < a.ring.service_waves) {
-      ring_service<FAM>(a, reinterpret_cast<float*>(svc_lds), svc_lds + 256, svc_lds + 512);
+      // a call (inlined, the service's registers pushed the march state into scratch), on the
+      // kernel arguments where they lie (a reference to the parameter copies it to scratch)
+      ring_service<FAM>(*(const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(),
+                        reinterpret_cast<uint32_t*>(&chunk_rays[0][0]));
       return;
     }
   }
@@ -617,11 +736,23 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
 #ifdef FRM_COUNT_EXACT
   uint64_t n_dbg_total = 0, n_dbg_exact = 0;
 #endif
+  uint32_t r_slot = 0;                    // RES: the slot of the wave's current chunk
   if constexpr (RES) {
     uint32_t b = 0;
-    if (lane == 0) b = max(a.ring.first_seq, dev_load(&a.ring.dev->base));
+    if (lane == 0) {
+      RING_GRID_TRACE(a.ring, 0);
+      b = max(a.ring.first_seq, dev_poll(&a.ring.dev->base));
+      ring_lds->host = a.ring.host;
+      ring_lds->dev = a.ring.dev;
+      ring_lds->order = a.ring.order;
+      ring_lds->slots = a.ring.slots;
+      ring_lds->grid_id = a.ring.grid_id;
+      ring_lds->rec_stride = a.rec_stride;
+      ring_lds->npix = a.npix;
+    }
+    __syncthreads();
     if (lane < (uint32_t)kRwWords) rw[lane] = 0u;
-    rw_set(rw, kRwSeq, uniform(__shfl(b, 0, 64)));
+    rw_set(rw, kRwLo, uniform(__shfl(b, 0, 64)));
   }
 
   // per-lane state
@@ -766,10 +897,6 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       closeness = kInfinity;
       FRM_SUB_END(2);
     }
-    if constexpr (RES) {  // count finished pixels per ring slot (ring_count_fins)
-      const uint64_t fm = ballot(fin);
-      if (fm) ring_count_fins(a, rw, fm, pix);
-    }
     if (fin) {  // primary miss (flags 0: BACKGROUND_COLOR) or end of the shadow march
       FRM_SUB_BEGIN();
       const uint32_t flags = ev_shadow ? (kRecHit | (sun_miss ? kRecSunMiss : 0u)) : 0u;
@@ -779,8 +906,14 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
         coherent_store(&tails[pix], tail);
       else
         *reinterpret_cast<uint2*>(&tails[pix]) = tail;
+      if constexpr (RES)  // the finished pixel into its slot's count (published by ring_settle)
+        atomicAdd(&rw[kRwPend + ring_slot_of(pix, rl_u32(ring_lds->rec_stride))], 1u);
       pix = kIdle;
       FRM_SUB_END(3);
+    }
+    if constexpr (RES) {  // drained slots whose last pixels left the lanes
+      const uint32_t gone = rw_get(rw, kRwGone);
+      if (gone) ring_settle(ring_lds, rw, gone, pix);
     }
     // 2. refill idle lanes from the wave's current chunk; fetch + ray-gen a new chunk
 #ifdef FRM_STAMPS
@@ -792,7 +925,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       if (slots_used == kChunk) {
         uint32_t base = kIdle;
         if constexpr (RES) {
-          base = ring_claim(a, rw, cam_lds, drained, part, nchunks, nhead);
+          base = ring_claim(ring_lds, rw, cam_lds, nchunks, nhead, pix, &r_slot);
         } else {
         // the head of the order (its most expensive chunks) from the shared counter
         if (!(drained >> kQueueParts)) {
@@ -836,6 +969,18 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
           uint32_t p = kIdle;
           v3 ray = mk(0.f, 0.f, 0.f);
           uint32_t pos0 = base, lim = total;
+          // RES: the chunk's frame's camera rows (wave-uniform, SGPRs): one LDS word per lane, then
+          // lane reads (twelve loads into VGPRs before their readfirstlanes pushed the march state
+          // into scratch). The load is pinned here, where every lane runs: the compiler would
+          // otherwise sink it into the branch below, and a lane read of a lane outside that
+          // branch's mask returns garbage.
+          [[maybe_unused]] float row[3][4];
+          if constexpr (RES) {
+            uint32_t mine = __float_as_uint(cam_lds[r_slot][lane & 15u]);
+            asm volatile("" : "+v"(mine));
+#pragma unroll
+            for (int i = 0; i < 12; ++i) row[i / 4][i % 4] = __uint_as_float(__builtin_amdgcn_readlane(mine, i));
+          }
           if constexpr (multi) {
             const uint32_t c = base / kChunk;
             chunk_frame = uniform(c % a.batch);
@@ -843,15 +988,17 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
             lim = a.npix;
           }
           if (pos0 + lane < lim) {
-            const uint32_t lp = RES ? a.ring.order[rw_get(rw, kRwSlot) * a.rec_stride + pos0 + lane] : a.pixel_order[pos0 + lane];
+            const uint32_t lp =
+                RES ? dev_load(&rl_ptr(((const volatile RingLds*)ring_lds)->order)[r_slot * a.rec_stride + pos0 + lane])
+                    : a.pixel_order[pos0 + lane];
             const uint32_t lr = lp / f.width, x = lp - lr * f.width, y = band_row_to_global(a.g, lr);
             if constexpr (RES)
-              ray = camera_ray_rows(f, *reinterpret_cast<const float(*)[3][4]>(cam_lds), x, y);
+              ray = camera_ray_rows(f, row, x, y);
             else if constexpr (multi)
               ray = camera_ray_rows(f, a.cams[chunk_frame].row, x, y);
             else
               ray = camera_ray(f, x, y);
-            p = (RES ? rw_get(rw, kRwSlot) * a.rec_stride : chunk_frame * a.rec_stride) + lp;  // the pixel's record index
+            p = (RES ? r_slot * a.rec_stride : chunk_frame * a.rec_stride) + lp;  // the pixel's record index
           }
           if constexpr (!RES) n_pix += count(p != kIdle);
           chunk_rays[wave][lane] = make_float4(ray.x, ray.y, ray.z, __uint_as_float(p));
@@ -861,6 +1008,14 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
       }
       if (slots_used < kChunk) {
         const uint32_t slot = slots_used + __popcll(want & (lane_bit - 1ull));
+        // RES: the chunk's frame's origin and power, read as the camera rows above
+        [[maybe_unused]] float cam_o[4];
+        if constexpr (RES) {
+          uint32_t mine = __float_as_uint(cam_lds[r_slot][12u + (lane & 3u)]);
+          asm volatile("" : "+v"(mine));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cam_o[i] = __uint_as_float(__builtin_amdgcn_readlane(mine, i));
+        }
         if ((want & lane_bit) && slot < kChunk) {
           const float4 r = chunk_rays[wave][slot];
           pix = __float_as_uint(r.w);
@@ -868,11 +1023,11 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
             pix_cost = 0;
             d = mk(r.x, r.y, r.z);
             if constexpr (RES)
-              o = mk(cam_lds[12], cam_lds[13], cam_lds[14]);
+              o = mk(cam_o[0], cam_o[1], cam_o[2]);
             else
               o = multi ? a.cams[chunk_frame].origin : f.origin;
             if constexpr (RES && ANIM)
-              lane_power = cam_lds[15];
+              lane_power = cam_o[3];
             else if constexpr (ANIM)
               lane_power = a.mb_powers[chunk_frame];
             t = 0.f;
@@ -930,7 +1085,7 @@ __global__ __launch_bounds__(kMarchBlock, FRM_MARCH_WAVES_PER_SIMD) void march_p
   if constexpr (RES) {
 #pragma unroll
     for (uint32_t sl = 0; sl < kRingSlots; ++sl)
-      if (sl < a.ring.slots) ring_flush(a, rw, sl);
+      if (sl < a.ring.slots) ring_flush(ring_lds, rw, sl);
   }
 
 #ifdef FRM_STAMPS

@@ -18,6 +18,12 @@ from helpers import params_for
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _ring_on(monkeypatch):
+    """The ring is opt-in (FRM_RING=1, read when a context is created)."""
+    monkeypatch.setenv("FRM_RING", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 W, H = 160, 90
 PERSISTENT = frm.FRM_FLAG_PERSISTENT_KERNEL

@@ -142,3 +142,29 @@ def test_v3_body_pow_no_less_accurate(oracle):
     # relative error: the largest ulp error sits where the f32 spacing is coarsest within a binade
     rel = lambda x: np.max(np.abs(x.astype(np.float64) - ref) / ref)  # noqa: E731
     assert rel(v3) <= 1.25 * rel(direct) and rel(v3) < 1e-5
+
+
+def test_v3_body_pow_within_wgsl_bound(oracle):
+    """frm v3's body pow, RN(pow(r, P - 1) * r), inside the bound WGSL gives pow(x, y): inherited
+    from exp2(y * log2(x)) (WGSL spec, "Floating Point Accuracy"), each step at its own f32 bound:
+    log2 x off by 3 ULP (absolute 2^-21 inside [0.5, 2]), the product rounded (1/2 ULP of z),
+    exp2 off by 3 + 2|z| ULP; an error dz in z moves the result by a factor 2^dz. Asserted per
+    element with P - 1 in place of y for the pow, plus 1/2 ULP for the product with r, on the body's
+    domain (r in [2^-13, 100], P in [4, 9])."""
+    rng = np.random.default_rng(7)
+    r = np.exp2(rng.uniform(-13, np.log2(100), 400000)).astype(np.float32)
+    p = rng.uniform(4, 9, 400000).astype(np.float32)
+    pm1 = (p - np.float32(1)).astype(np.float32)
+    v3 = (oracle.math_fn("pow", r, pm1).astype(np.float32) * r).astype(np.float32).astype(np.float64)
+    r64, y = r.astype(np.float64), pm1.astype(np.float64)
+    ref = np.power(r64, p.astype(np.float64))
+    l2 = np.log2(r64)
+    inside = (r64 >= 0.5) & (r64 <= 2.0)
+    e_log2 = np.where(inside, 2.0 ** -21, 3 * np.spacing(np.abs(l2).astype(np.float32)).astype(np.float64))
+    z = y * l2
+    dz = np.abs(y) * e_log2 + 0.5 * np.spacing(np.abs(z).astype(np.float32)).astype(np.float64)
+    ulp = 2.0 ** -23  # relative size of one ULP, at most
+    bound = (np.exp2(dz) - 1) + (3 + 2 * np.abs(z)) * ulp + 0.5 * ulp
+    rel = np.abs(v3 - ref) / ref
+    assert np.all(rel <= bound), float(np.max(rel / bound))
+    assert np.max(rel / bound) < 0.5  # measured: at most 0.236 of the budget

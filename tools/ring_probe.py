@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--fif", type=int, default=2)
     ap.add_argument("--loops", default="latency,noread,wait")
-    ap.add_argument("--modes", default="1,0", help="FRM_RING values to run (1: ring, 0: per-frame grids)")
+    ap.add_argument("--modes", default="1,0", help="FRM_RING values to run (1: the ring, 0: per-frame grids, the default)")
     ap.add_argument("--child", action="store_true")
     args = ap.parse_args()
     if args.child:
