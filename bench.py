@@ -88,6 +88,9 @@ def parse():
                     "gated by tests/test_gpu_hw_math.py; a separate line, never the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in loop measurement (dropin_ms_per_frame)")
+    ap.add_argument("--dropin-only", action="store_true",
+                    help="internal: only the drop-in loop (2 in flight, a frame of latency), one JSON line; "
+                    "bench.py runs it as a child at HIP's default 4 hardware queues (dropin_q4)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--reload", default=None, help="render with kernels recompiled at run time from this "
                     "copy of csrc/ (frm_reload, hiprtc)")
@@ -210,7 +213,7 @@ def pmc_summary(workload, world, math="exact"):
     return {"stale": stale, "source_sha256": cur} if stale else None
 
 
-def dropin_loop(frm, torch, w, args, flags, local, camera):
+def dropin_loop(frm, torch, w, args, flags, local, camera, forms=(("dropin", 2, 1), ("dropin_sync", 1, 0))):
     """The drop-in binding's frame loop, measured in the same run: one
     frm_render per frame with that frame's Parameters (frm.frame_sequence, as bench's timed
     region), every frame read back to the host (the reference presents every frame,
@@ -228,7 +231,8 @@ def dropin_loop(frm, torch, w, args, flags, local, camera):
     n = max(1, min(args.steps, 30))
     frames = [next(seq) for _ in range(n)] if w.moving else [next(seq)] * n
     out = {}
-    for name, fif, lag in (("dropin", 2, 1), ("dropin_sync", 1, 0)):
+    steps = kernel_ms = 0  # the march steps of the frames (the dropin form's stats pass; same frames in both)
+    for name, fif, lag in forms:
         with frm.Renderer(device=local, max_steps=w.max_steps, flags=flags, frames_in_flight=fif) as r:
             r.resize(w.width, w.height)
             r.update_parameters_buffer(frames[0])
@@ -247,22 +251,49 @@ def dropin_loop(frm, torch, w, args, flags, local, camera):
             for t in held:
                 r.frame_pixels(t, copy=False)
             dt = time.perf_counter() - t0
-            if name == "dropin":
-                steps = kernel_ms = 0
+            if name == "dropin" and not args.dropin_only:
                 for p in frames:
                     r.update_parameters_buffer(p)
                     st = r.render(stats=True)
                     steps += st["march_steps"]
                     kernel_ms += st["kernel_ms"]
         out[f"{name}_ms_per_frame"] = dt / n * 1e3
-        out[name] = {"frames": n, "value": steps / dt / 1e9, "unit": "Gray-march-steps/s",
+        out[name] = {"frames": n, "value": steps / dt / 1e9 if steps else None, "unit": "Gray-march-steps/s",
                      "frames_in_flight": fif, "frames_per_launch": 1, "present_latency_frames": lag,
                      "loop": ("frm_render + frm_read_frame_async per frame, frm_frame_pixels of the previous "
                               "frame (INTEGRATION.md section 3)" if lag else
                               "frm_render + readback per frame, host waits for each frame")}
-        if name == "dropin":
+        if name == "dropin" and steps:
             out[name]["kernel_ms_per_frame_alone"] = kernel_ms / n
     return out
+
+
+def dropin_q4(args):
+    """The drop-in loop at HIP's default GPU_MAX_HW_QUEUES=4 (a host that does not raise it, e.g. a
+    Rust binding), in a child process: the queue count is fixed when HIP starts, and this process
+    runs at 16. None when the child fails."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--dropin-only", "--hw-queues", "4", "--workload", args.workload,
+           "--pose", args.pose, "--steps", str(args.steps), "--kernel", args.kernel, "--math", args.math]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        return json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else None
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        return None
+
+
+def dropin_only(args):
+    import torch
+
+    import frm
+
+    w = frm.WORKLOADS[args.workload]
+    flags = (frm.FRM_FLAG_SCENE_SPHERE if w.sphere else 0) | (
+        {"auto": 0, "simple": frm.FRM_FLAG_SIMPLE_KERNEL, "persistent": frm.FRM_FLAG_PERSISTENT_KERNEL}[args.kernel]) | (
+        frm.FRM_FLAG_HW_MATH if args.math == "hw" else 0)
+    torch.cuda.set_device(0)
+    out = dropin_loop(frm, torch, w, args, flags, 0, None, forms=(("dropin", 2, 1),))
+    print(json.dumps({"dropin_ms_per_frame": out["dropin_ms_per_frame"],
+                      "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])}))
 
 
 def launch_ranks(args):
@@ -434,6 +465,9 @@ def main():
     args = parse()
     if args.mode == "group":
         return group_bench(args)
+    if args.dropin_only:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues or 4)
+        return dropin_only(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args)
     # before torch initialises HIP
@@ -616,6 +650,8 @@ def main():
     dropin = None
     if world == 1 and not args.no_dropin:
         dropin = dropin_loop(frm, torch, w, args, flags, local, camera)
+        if int(os.environ["GPU_MAX_HW_QUEUES"]) != 4:
+            dropin["dropin_q4"] = dropin_q4(args)
 
     stats_vec = torch.tensor([elapsed, span_ms], dtype=torch.float64, device=dev)
     cnt = counters.clone()

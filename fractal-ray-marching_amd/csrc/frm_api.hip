@@ -95,10 +95,16 @@ struct Slot {
   bool order_ready = false;
   uint64_t order_key = 0;
   // asynchronous readback (frm_read_frame_async / frm_present_async): the frame's bytes (or its
-  // blit) copied into a pinned host image on the slot's copy stream, after the render (`done`);
-  // `copied` is recorded after the copy, and the slot's next frm_render waits for it before its
-  // launch rewrites the framebuffer. The render stream itself goes straight on to the next frame.
-  hipStream_t copy_stream = nullptr;
+  // blit) copied into a pinned host image after the render, on `rb_stream`: the render's own stream
+  // when frames are in flight (another slot's stream renders the next frame meanwhile), else the
+  // slot's copy stream after `done`, so that a lone slot's stream goes straight on to the next frame.
+  // One stream per slot keeps a context within HIP's default 4 hardware queues per process: with a
+  // copy stream per slot as well, 2 frames in flight used 4 streams, queues were shared and a
+  // frame's render queued behind the previous frame's copy (drop-in loop at
+  // GPU_MAX_HW_QUEUES=4). `copied` is recorded after the copy; the slot's next frm_render waits for
+  // it before its launch rewrites the framebuffer.
+  hipStream_t copy_stream = nullptr;  // owned (one slot only)
+  hipStream_t rb_stream = nullptr;    // the stream of the last readback's copy
   uint8_t* host_img = nullptr;
   size_t host_cap = 0;
   uint8_t* present_dev = nullptr;  // frm_present_async's blit output (device, context pool), grown on demand
@@ -1456,13 +1462,18 @@ int frm_present(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uint32_t 
 
 // The slot's copy stream, ordered after the slot's last launch (its render).
 static int copy_stream_after_render(frm_ctx* ctx, Slot& sl) {
+  if (ctx->nslots >= 2 && sl.last_stream) {  // stream order: after the render
+    sl.rb_stream = sl.last_stream;
+    return FRM_OK;
+  }
   if (!sl.copy_stream) FRM_HIP(ctx, hipStreamCreateWithFlags(&sl.copy_stream, hipStreamNonBlocking));
   FRM_HIP(ctx, hipStreamWaitEvent(sl.copy_stream, sl.done, 0));
+  sl.rb_stream = sl.copy_stream;
   return FRM_OK;
 }
 
 // Enqueues the copy of `bytes` device bytes of the last frm_render's slot into its pinned host
-// image (on the slot's copy stream, after copy_stream_after_render) and hands out a ticket for it.
+// image (on sl.rb_stream, after copy_stream_after_render) and hands out a ticket for it.
 static int readback_async(frm_ctx* ctx, Slot& sl, const uint8_t* src, size_t bytes, uint64_t* out_ticket) {
   if (bytes > sl.host_cap) {
     // the image's previous contents belong to an expired ticket (an earlier frame of this slot);
@@ -1477,10 +1488,10 @@ static int readback_async(frm_ctx* ctx, Slot& sl, const uint8_t* src, size_t byt
     FRM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&sl.host_img), cap, hipHostMallocDefault));
     sl.host_cap = cap;
   }
-  FRM_HIP(ctx, hipMemcpyAsync(sl.host_img, src, bytes, hipMemcpyDeviceToHost, sl.copy_stream));
-  FRM_HIP(ctx, hipEventRecord(sl.copied, sl.copy_stream));
+  FRM_HIP(ctx, hipMemcpyAsync(sl.host_img, src, bytes, hipMemcpyDeviceToHost, sl.rb_stream));
+  FRM_HIP(ctx, hipEventRecord(sl.copied, sl.rb_stream));
   // the framebuffer is read (by this copy, or by frm_present_async's blit before it) until here
-  FRM_HIP(ctx, hipEventRecord(sl.fb_read[sl.fb_idx], sl.copy_stream));
+  FRM_HIP(ctx, hipEventRecord(sl.fb_read[sl.fb_idx], sl.rb_stream));
   sl.fb_read_pending[sl.fb_idx] = true;
   sl.copy_ticket = ++ctx->ticket_seq;
   sl.copy_bytes = bytes;
@@ -1513,15 +1524,16 @@ int frm_present_async(frm_ctx* ctx, uint32_t out_width, uint32_t out_height, uin
   const size_t need = (size_t)out_width * out_height * 4u;
   int rc = copy_stream_after_render(ctx, sl);
   if (rc) return rc;
-  if (need > sl.present_dev_cap) {  // its last use (an earlier frame of this slot) is ordered before, on the copy stream
-    if ((rc = dev_release(ctx, sl.present_dev, sl.copy_stream))) return rc;
+  if (need > sl.present_dev_cap) {  // its last use (an earlier frame of this slot) is ordered before
+    if (sl.copy_ticket && sl.rb_stream) FRM_HIP(ctx, hipEventSynchronize(sl.copied));  // maybe on another stream
+    if ((rc = dev_release(ctx, sl.present_dev, sl.rb_stream))) return rc;
     sl.present_dev = nullptr;
     sl.present_dev_cap = 0;
-    if ((rc = dev_alloc(ctx, (void**)&sl.present_dev, need, sl.copy_stream))) return rc;
+    if ((rc = dev_alloc(ctx, (void**)&sl.present_dev, need, sl.rb_stream))) return rc;
     sl.present_dev_cap = need;
   }
   FRM_HIP(ctx, launch_blit(sl.fb, ctx->width, ctx->height, sl.present_dev, out_width, out_height, flags,
-                           sl.copy_stream));
+                           sl.rb_stream));
   return readback_async(ctx, sl, sl.present_dev, need, out_ticket);
 }
 
