@@ -798,7 +798,6 @@ __global__ __launch_bounds__(kMarchBlock, RES ? FRM_RING_WAVES_PER_SIMD : FRM_MA
 #ifdef FRM_STAMPS
         n_loop++;
 #endif
-        uint32_t fin = 0;
         if (lane_in(pending)) {
 #if defined(FRM_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostic: body-loop iterations, and those that ran the exact body
           n_dbg_total++;
@@ -809,14 +808,12 @@ __global__ __launch_bounds__(kMarchBlock, RES ? FRM_RING_WAVES_PER_SIMD : FRM_MA
           else
             mb_step<kHw>(su, q, mag, z, dr);
           body++;
-          if (body > n_iter) {
-            fin = 1;  // N+1 bodies: the distance uses the last loop-top magnitude
-          } else {
-            mag = mb_length<kHw>(z);
-            fin = mag > su.mb_bailout;
-          }
+          // N+1 bodies: the distance uses the last loop-top magnitude
+          if (body <= n_iter) mag = mb_length<kHw>(z);
         }
-        pending &= ~ballot(fin != 0);
+        // the lanes whose DE ends, tested by every lane outside the body's branch (other lanes'
+        // bits fall outside `pending`): a flag set inside it reached the mask through a VGPR
+        pending &= ~(ballot(body > n_iter) | ballot(mag > su.mb_bailout));
       }
       done = !lane_in(pending);  // idle lanes: masked by cons
     }
