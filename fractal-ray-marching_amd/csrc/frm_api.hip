@@ -42,7 +42,14 @@ static constexpr uint64_t kQueueHeadroom = 1ull << 24;
 // 16 = half the 8-wave kernel's occupancy (sweep 12/14/16/32 on the drop-in loop: 8.22 / 8.03 /
 // 7.90 / 8.55 ms fixed, 8.96 / 8.82 / 8.71 / 9.87 moving; profiles/round5/dropin_bpc8; with the
 // round-5 7-wave kernel 12 was best, profiles/round5/dropin_bpc).
+// With F frames in flight the cap is the kernel's occupancy (32 workgroups per CU) over F, so the F
+// grids fit side by side (round 6, one rank's 8-way share of the headline, one frame per launch:
+// 3 in flight 1.49 ms at 16 per CU, 1.21 at 10-11; 4 in flight 1.09 at 8; 2 in flight 16 stays best,
+// 1.53-1.56 at 12-20; profiles/round6/share/). F = 2 gives the 16 above.
 static constexpr int kInflightBlocksPerCu = 16;
+static int inflight_blocks_per_cu(uint32_t frames_in_flight) {
+  return frames_in_flight <= 2u ? kInflightBlocksPerCu : (int)(2u * kInflightBlocksPerCu / frames_in_flight);
+}
 static constexpr uint64_t kInflightCapPixels = 4ull * 3840u * 2160u;
 // Single-frame launches with one frame in flight: 7 waves/SIMD (28 one-wave workgroups per CU)
 // rather than the kernel's 8. A lone frame ends with its costliest pixels' marches, which an
@@ -560,7 +567,7 @@ int launch(frm_ctx* ctx, KernelArgs a, hipStream_t s, uint32_t* out_slot = nullp
   int blocks_cap = 0;
   if (a.batch == 1) {
     if (ctx->nslots >= 2 && a.npix <= kInflightCapPixels)
-      blocks_cap = kInflightBlocksPerCu;
+      blocks_cap = inflight_blocks_per_cu(ctx->nslots);
     else if (ctx->nslots == 1)
       blocks_cap = kLoneFrameBlocksPerCu;
   }
