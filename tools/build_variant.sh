@@ -5,6 +5,7 @@
 # call ships it.
 # Usage: PATCH=profiles/round4/ab_prio/prio.patch bash tools/build_variant.sh NAME "-DFOO=1 ..."
 # (SCHEDFLAGS=... in the environment replaces the Makefile's scheduler options, e.g. SCHEDFLAGS="")
+# (MAKEVARS="RING_WAVES=8 ..." passes Makefile variables)
 set -e
 NAME=$1; FLAGS=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -18,7 +19,7 @@ if [ -n "$PATCH" ]; then
 fi
 OBJ=build/obj_$NAME
 mkdir -p ab
-make -s CSRC="$SRC" OBJDIR=$OBJ EXTRA_HIPFLAGS="$FLAGS" ${SCHEDFLAGS+SCHEDFLAGS="$SCHEDFLAGS"} $OBJ/frm_kernels.o $OBJ/frm_api.o \
+make -s CSRC="$SRC" OBJDIR=$OBJ EXTRA_HIPFLAGS="$FLAGS" $MAKEVARS ${SCHEDFLAGS+SCHEDFLAGS="$SCHEDFLAGS"} $OBJ/frm_kernels.o $OBJ/frm_api.o \
   $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ab/$NAME.so $OBJ/frm_kernels.o \
   $OBJ/frm_api.o $OBJ/frm_sched.o $OBJ/frm_host.o $OBJ/frm_reload.o -lhiprtc -lrccl
