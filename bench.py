@@ -651,7 +651,9 @@ def main():
     if world == 1 and not args.no_dropin:
         dropin = dropin_loop(frm, torch, w, args, flags, local, camera)
         if int(os.environ["GPU_MAX_HW_QUEUES"]) != 4:
-            dropin["dropin_q4"] = dropin_q4(args)
+            q4 = dropin_q4(args)
+            dropin["dropin_q4_ms_per_frame"] = q4["dropin_ms_per_frame"] if q4 else None
+            dropin["dropin_q4"] = q4
 
     stats_vec = torch.tensor([elapsed, span_ms], dtype=torch.float64, device=dev)
     cnt = counters.clone()
