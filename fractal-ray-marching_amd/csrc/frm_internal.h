@@ -71,6 +71,8 @@ constexpr uint32_t kQueuePartWords = 64;    // u32 words between two counters (2
 constexpr uint32_t kQueueDebugWord = (kQueueParts + 1u) * kQueuePartWords;  // FRM_STAMPS words after the counters
 constexpr size_t kQueueBytes = (kQueueDebugWord + 64u) * 4u;
 constexpr uint32_t kMarchWaves = kMarchBlock / 64u;
+// KernelArgs::first_info bits: the frame skips step 0 / the step exited by bailout / its cost
+constexpr uint32_t kFirstSkip = 1u << 31, kFirstBail = 1u << 30, kFirstCostMask = (1u << 30) - 1u;
 constexpr uint32_t kRankWords = 512;  // one launch's key_hist: 256 counts + 256 cursors
 constexpr uint32_t kShadeBlockPixels = 4096;  // shade_pass / rank_pass: local pixels per 256-thread block
 
@@ -196,6 +198,16 @@ struct KernelArgs {
   // only: fragment.wgsl:75): frame k's power. Used by the ANIM instantiation of march_persistent,
   // which carries a per-lane power; s.mb_power otherwise.
   float mb_powers[kMaxBatch];
+  // Step 0 of frame k's primary rays (launch_persistent, built-in kernels; 0 = none): every one
+  // samples ray_at(origin, 0, dir) = origin, the same point for all the frame's pixels, so its DE
+  // is evaluated once on the host with the kernels' own source (frm_scene.h, bit-identical to the
+  // device: tests/native) and each fetched pixel starts at step 1 with t = first_t[k].
+  // first_info[k]: the step's cost (Mandelbulb bodies, else 1 DE) | kFirstBail | kFirstSkip.
+  float first_t[kMaxBatch];
+  uint32_t first_info[kMaxBatch];
+  // the skipped steps' counts over the launch (primary DEs, Mandelbulb bodies, bailouts), added to
+  // the counters once by the first wave
+  unsigned long long first_counts[3];
   uint32_t anim;
   RingArgs ring;  // march_persistent<..., RES = true>: the resident frame ring
 };

@@ -7,6 +7,8 @@
 // active (frm_reload.hip).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "frm_render_kernels.h"
 
 namespace frm {
@@ -158,6 +160,48 @@ static hipError_t module_launch(hipFunction_t fn, dim3 grid, dim3 block, hipStre
   return hipModuleLaunchKernel(fn, grid.x, grid.y, grid.z, block.x, block.y, block.z, 0, stream, params, nullptr);
 }
 
+// KernelArgs::first_t / first_info: step 0 of each frame's primary rays, evaluated here once per
+// frame instead of once per pixel (fragment.wgsl:289-300 at total_distance 0: ray_at(o, 0, d) =
+// fma(0, d, o) = o bit for bit, unless a component of o is -0, whose sum with 0 * d would follow
+// d's sign). The DE is the kernels' own scene_de built for the host (the exact builtins; the
+// device's tame paths give the same bits, tests/native and test_gpu_de), with the power the march
+// uses (ANIM: the frame's power, power - 1). The pixels skip the step only when it neither hits
+// nor ends the march (distance in (MIN_DISTANCE, MAX_TOTAL_DISTANCE), max_steps >= 2): they then
+// start at step 1 with t = 0 + distance, it = 1, the step's bodies in their cost and the step
+// counted (primary DE, bodies, bailout) as its consumption would. Not for hardware math (no host
+// equivalent) or runtime-reloaded kernels (edited sources).
+template <uint32_t FAM, bool ITERS>
+static void first_steps(KernelArgs& a, bool anim) {
+  a.first_counts[0] = a.first_counts[1] = a.first_counts[2] = 0;
+  if constexpr (FAM == kMandelbulbHw) {
+    (void)anim;
+  } else {
+    for (uint32_t k = 0; k < a.batch && k < kMaxBatch; ++k) {
+      const v3 o = a.cams[k].origin;
+      SceneUniforms u = a.s;
+      if (anim) {
+        u.mb_power = a.mb_powers[k];
+        u.mb_power_m1 = u.mb_power - 1.0f;
+      }
+      DeCount cnt = {0u, 0u};
+      const float de = scene_de<FAM, ITERS>(u, o, cnt);
+      uint32_t ob[3];
+      memcpy(ob, &o, sizeof(ob));
+      const bool neg0 = ob[0] == 0x80000000u || ob[1] == 0x80000000u || ob[2] == 0x80000000u;
+      const bool skip = !neg0 && a.f.max_steps >= 2u && de > kMinDistance && de < kMaxTotalDistance;
+      a.first_t[k] = 0.0f + de;
+      a.first_info[k] = skip ? ((is_mandelbulb(FAM) ? cnt.bodies : 1u) | (cnt.bailouts ? kFirstBail : 0u) | kFirstSkip) : 0u;
+      if (skip) {  // every local pixel of the frame is fetched once by this launch
+        a.first_counts[0] += a.npix;
+        if (is_mandelbulb(FAM)) {
+          a.first_counts[1] += (unsigned long long)a.npix * cnt.bodies;
+          a.first_counts[2] += cnt.bailouts ? a.npix : 0u;
+        }
+      }
+    }
+  }
+}
+
 // Every built-in persistent launch, a single frame included, runs the multi-frame instantiation
 // (a single frame is a batch of one, its camera in cams[0]): the single-frame one needs 82 VGPRs
 // on ROCm 7.2 (5 waves/SIMD), the multi-frame one 80 (6 waves/SIMD).
@@ -196,14 +240,17 @@ static hipError_t launch_persistent(const KernelArgs& args, int cu_count, hipStr
     if (e != hipSuccess) return e;
     return module_launch(rk->shade[FAM], dim3(shade_blocks, args.batch), dim3(256), stream, args);
   }
-  if constexpr (is_mandelbulb(FAM) && ITERS) {
+  KernelArgs m = args;  // + the frames' step 0
+  constexpr bool kAnimKernel = is_mandelbulb(FAM) && ITERS;  // the ANIM instantiation exists
+  first_steps<FAM, ITERS>(m, kAnimKernel && args.anim);
+  if constexpr (kAnimKernel) {
     if (args.anim) {
-      hipLaunchKernelGGL((march_persistent<FAM, ITERS, true, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+      hipLaunchKernelGGL((march_persistent<FAM, ITERS, true, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, m);
     } else {
-      hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+      hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, m);
     }
   } else {
-    hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, args);
+    hipLaunchKernelGGL((march_persistent<FAM, ITERS, true>), dim3(blocks), dim3(kMarchBlock), 0, stream, m);
   }
   hipLaunchKernelGGL((shade_pass<FAM>), dim3(shade_blocks, args.batch), dim3(256), 0, stream, args);
   if (args.key_hist)  // fused scheduling: the slot's next fetch order

@@ -1017,7 +1017,11 @@ __global__ __launch_bounds__(kMarchBlock, RES ? FRM_RING_WAVES_PER_SIMD : FRM_MA
           const float4 r = chunk_rays[wave][slot];
           pix = __float_as_uint(r.w);
           if (pix != kIdle) {
-            pix_cost = 0;
+            // the frame's step 0 done once (KernelArgs::first_info; ring frames run it per pixel):
+            // start at step 1 where consuming it would leave the pixel
+            const uint32_t fy = RES ? 0u : a.first_info[chunk_frame];
+            const bool first_skip = (fy & kFirstSkip) != 0u;
+            pix_cost = first_skip ? (fy & kFirstCostMask) : 0u;
             d = mk(r.x, r.y, r.z);
             if constexpr (RES)
               o = mk(cam_o[0], cam_o[1], cam_o[2]);
@@ -1027,8 +1031,8 @@ __global__ __launch_bounds__(kMarchBlock, RES ? FRM_RING_WAVES_PER_SIMD : FRM_MA
               lane_power = cam_o[3];
             else if constexpr (ANIM)
               lane_power = a.mb_powers[chunk_frame];
-            t = 0.f;
-            it = 0;
+            t = first_skip ? a.first_t[chunk_frame] : 0.f;
+            it = first_skip ? 1u : 0u;
             phase = kPrimary;
             need_point = true;
           }
@@ -1118,6 +1122,11 @@ __global__ __launch_bounds__(kMarchBlock, RES ? FRM_RING_WAVES_PER_SIMD : FRM_MA
 #ifdef FRM_COUNT_EXACT
     atomicAdd(&a.counters[7], (unsigned long long)((n_dbg_total << 32) | n_dbg_exact));
 #endif
+    if (blockIdx.x == 0 && wave == 0) {  // the launch's skipped steps 0 (KernelArgs::first_counts)
+      n_prim += a.first_counts[0];
+      n_body += a.first_counts[1];
+      n_bail += a.first_counts[2];
+    }
     unsigned long long v[7] = {n_pix, n_hit, n_prim, n_shadow, 4ull * n_hit, n_body, n_bail};
 #pragma unroll
     for (int k = 0; k < 7; ++k)

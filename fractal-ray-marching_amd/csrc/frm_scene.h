@@ -320,14 +320,17 @@ __device__ __forceinline__ bool lane_in(uint64_t mask) {
 // min/max(|x|,|y|) are tame divisions, log2(r) has a positive normal argument and the
 // exp2 argument (P-1)*log2 r (P in [4, 9], log2 r in [-13, log2 100]) lies in [-104, 54],
 // where exp2_tame's result is normal (and so is its product with r, pow(r, P): >= 2^-117).
-// Branch-free: (bits << 1) - 1 drops the sign and maps +-0 to UINT_MAX, so one unsigned
-// min3 + compare tests "0 or |v| >= 2^-60" for the three components at once (NaN
-// components also pass, but then r is NaN and fails r >= 2^-40).
-__device__ __forceinline__ uint32_t comp_key(float v) { return (__float_as_uint(v) << 1) - 1u; }
+// The test is stricter than that domain: every |component| >= 2^-60 (one v_min3_f32 with |.|
+// modifiers; a NaN component loses the minNum, but then r is NaN and fails r >= 2^-13), so an exact
+// zero component also takes the exact body (same bits, slower). Such zeros came from step 0 of the
+// primary rays, which samples the camera origin itself (P1: (0, 0, -1.6)): 14.5 % of body-loop
+// iterations went exact (profiles/round6/ab_tame). That step now runs once per frame on the host
+// (frm_kernels.hip first_steps), and the headline's body loop runs no exact body at all; the
+// integer-key test that let zeros pass cost 3 VALU more per iteration.
 __device__ __forceinline__ bool mb_tame(v3 z, float r) {
-  constexpr uint32_t kMin = (0x21800000u << 1) - 1u;  // comp_key(0x1p-60f)
-  const uint32_t m = min(min(comp_key(z.x), comp_key(z.y)), comp_key(z.z));  // v_min3_u32
-  return (r >= 0x1p-13f) & (m >= kMin);
+  float m;
+  asm("v_min3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m) : "v"(z.x), "v"(z.y), "v"(z.z));
+  return (r >= 0x1p-13f) & (m >= 0x1p-60f);
 }
 
 // mb_body (frm_scene.h) with the tame primitives: the same operations in the same order.

@@ -115,3 +115,26 @@ def test_kernel_choice(gpu_renderer_factory):
     for bad in (frm.FRM_FLAG_SIMPLE_KERNEL | frm.FRM_FLAG_PERSISTENT_KERNEL, 0x80):
         with pytest.raises(frm.FrmError):
             gpu_renderer_factory(flags=bad)
+
+
+@pytest.mark.parametrize("scene,iters,time", [(18, 12, frm.POWER8_TIME), (0, 3, 0.0)], ids=["mandelbulb", "menger"])
+def test_step0_once_per_frame_edge_cases(gpu_renderer_factory, oracle, scene, iters, time):
+    """Step 0 of the primary rays is evaluated once per frame on the host (frm_kernels.hip
+    first_steps) and skipped per pixel only when it neither hits nor ends the march and the
+    origin has no -0 component. Each case below takes the other branch or an edge of it; bytes
+    and counters equal the oracle's either way."""
+    cases = [
+        ((-0.0, 0.0, -1.6), 0.0, 0.0, 64),    # -0 component: 0 * d would follow d's sign, no skip
+        ((0.0, -0.0, -1.6), 0.2, 0.1, 64),
+        ((0.0, 0.0, -1.6), 0.0, 0.0, 1),      # one step: step 0 ends the march, no skip
+        ((0.0, 0.0, -1.6), 0.0, 0.0, 2),      # two steps: skip, then the last step
+        ((0.0, 0.0, -1500.0), 0.0, 0.0, 64),  # step 0's distance beyond MAX_TOTAL_DISTANCE: no skip
+        ((0.3, -0.2, -2.5), 0.4, -0.3, 64),   # no zero component
+    ]
+    for pos, yaw, pitch, steps in cases:
+        p = params_for(scene, iters, time, 48, 27)
+        p.update_camera(frm.Camera(pos, yaw, pitch))
+        img, st = gpu_render(gpu_renderer_factory, p, 48, 27, steps, frm.FRM_FLAG_PERSISTENT_KERNEL)
+        ref = oracle.render(p, 48, 27, steps)
+        assert np.array_equal(img, ref["rgba"]), (pos, steps)
+        assert counters_of(st) == [int(c) for c in ref["counters"]], (pos, steps)
